@@ -1,0 +1,166 @@
+/*
+ * khmer_hip.h -- C ABI of libkhmer_hip.so, the MI355X-native k-mer counting
+ * engine behind the khmer_amd Python package.
+ *
+ * Plain pointers and sizes only; no torch types.  Each entry point names the
+ * reference interface it replaces (paths under ctb/khmer).  Every function
+ * returns a status code (KH_OK on success); on failure kh_last_error() holds a
+ * thread-local message and the code selects the Python exception class the
+ * reference raises for the same failure
+ * (khmer/_oxli/oxli_exception_convert.cc:9-31).
+ *
+ * Threading: calls on one graph are serialised by the library (the reference's
+ * atomic/spin-locked table updates, include/oxli/storage.hh:571-624); a parser
+ * may be drained by several threads, each read is consumed exactly once
+ * (src/oxli/read_parsers.cc:329-372).  ctypes releases the GIL around calls.
+ */
+#ifndef KHMER_HIP_H
+#define KHMER_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KH_ABI_VERSION 1
+
+/* status codes -> Python exceptions */
+#define KH_OK       0
+#define KH_EVALUE   1  /* ValueError    (oxli_value_exception, InvalidValue, InvalidRead) */
+#define KH_EFILE    2  /* OSError       (oxli_file_exception, InvalidStream, StreamReadError) */
+#define KH_EATTR    3  /* AttributeError (ReadOnlyAttribute) */
+#define KH_ENOMEM   4  /* MemoryError   (std::bad_alloc, hipErrorOutOfMemory) */
+#define KH_EDEVICE  5  /* RuntimeError  (HIP runtime failure / no device) */
+#define KH_ERUNTIME 6  /* RuntimeError  (generic oxli_exception in helpers) */
+#define KH_END      7  /* not an error: parser exhausted (NoMoreReadsAvailable) */
+
+/* storage kinds == on-disk type codes (include/oxli/oxli.hh:91-97) */
+#define KH_STORAGE_BYTE   1  /* ByteStorage   -> Countgraph / Counttable           */
+#define KH_STORAGE_BIT    2  /* BitStorage    -> Nodegraph / Nodetable             */
+#define KH_STORAGE_NIBBLE 7  /* NibbleStorage -> SmallCountgraph / SmallCounttable */
+
+/* hash families */
+#define KH_HASH_TWOBIT 0  /* Hashgraph: reversible 2-bit (include/oxli/kmer_hash.hh:62-96) */
+#define KH_HASH_MURMUR 1  /* MurmurHashtable (include/oxli/hashtable.hh:494-534)           */
+
+typedef struct kh_graph kh_graph;
+typedef struct kh_parser kh_parser;
+
+const char *kh_last_error(void);
+int kh_abi_version(void);
+/* number of visible HIP devices (0 when none; never an error) */
+int kh_device_count(int *n);
+
+/* ---------------- hashing helpers ------------------------------------------
+ * replaces khmer._khmer.forward_hash / forward_hash_no_rc / reverse_hash /
+ * hash_murmur3 / hash_no_rc_murmur3 / reverse_complement
+ * (src/khmer/_cpy_khmer.cc:63-190 over src/oxli/kmer_hash.cc:65-207) */
+int kh_hash_twobit(const char *kmer, int k, uint64_t *fwd, uint64_t *rc, uint64_t *canon);
+int kh_reverse_hash(uint64_t h, int k, char *out /* k+1 */);
+int kh_hash_murmur(const char *kmer, int len, uint64_t *canon, uint64_t *fwd);
+int kh_reverse_complement(const char *s, size_t len, char *out /* len+1 */);
+/* all k-mer hashes of a string, reference iterator semantics
+ * (Hashtable::get_kmer_hashes, src/oxli/hashtable.cc:378-388) */
+int kh_kmer_hashes(int hash_kind, int k, const char *seq, size_t len,
+                   uint64_t *out, uint64_t *n_out);
+
+/* ---------------- primes ----------------------------------------------------
+ * replaces khmer._oxli.utils.get_n_primes_near_x / is_prime
+ * (khmer/_oxli/utils.pyx:12-17 over include/oxli/hashtable.hh:79-123) */
+int kh_is_prime(uint64_t n, int *out);
+int kh_get_n_primes_near_x(uint32_t n, uint64_t x, uint64_t *out, uint32_t *found);
+
+/* ---------------- read parser -----------------------------------------------
+ * replaces oxli::read_parsers::ReadParser<FastxReader> and the CPython
+ * khmer.ReadParser (include/oxli/read_parsers.hh:138-178,
+ * src/oxli/read_parsers.cc:257-382, src/khmer/_cpy_readparsers.cc:392-550).
+ * FASTA/FASTQ, plain or gzip. */
+int  kh_parser_open(const char *path, kh_parser **out);
+/* next read; returns KH_END when exhausted.  Pointers stay valid until the
+ * next call on this parser from the same thread. */
+int  kh_parser_next_read(kh_parser *p, const char **name, size_t *name_len,
+                         const char **seq, size_t *seq_len,
+                         const char **qual, size_t *qual_len);
+int  kh_parser_num_reads(kh_parser *p, uint64_t *out);
+int  kh_parser_is_complete(kh_parser *p, int *out);
+void kh_parser_close(kh_parser *p);
+
+/* ---------------- graph lifecycle -------------------------------------------
+ * replaces the Countgraph / SmallCountgraph / Nodegraph (and Counttable /
+ * SmallCounttable / Nodetable) constructors, khmer/_oxli/graphs.pyx:817-900 ->
+ * include/oxli/hashgraph.hh:273-296, include/oxli/hashtable.hh:591-627.
+ * Tables live in HBM of `device`; they are zero-initialised. */
+int  kh_graph_create(int storage, int hash_kind, int k, const uint64_t *sizes,
+                     int n_tables, int device, kh_graph **out);
+void kh_graph_destroy(kh_graph *g);
+int  kh_graph_info(kh_graph *g, int *storage, int *hash_kind, int *k, int *n_tables);
+int  kh_graph_tablesizes(kh_graph *g, uint64_t *out);          /* hashsizes() */
+int  kh_graph_set_use_bigcount(kh_graph *g, int on);           /* storage.cc:50-56 */
+int  kh_graph_get_use_bigcount(kh_graph *g, int *on);
+int  kh_graph_n_unique_kmers(kh_graph *g, uint64_t *out);      /* storage.hh:143-165 */
+int  kh_graph_n_occupied(kh_graph *g, uint64_t *out);
+/* largest k-mer batch processed per device pipeline pass (memory knob) */
+int  kh_graph_set_batch_kmers(kh_graph *g, uint64_t max_kmers);
+
+/* ---------------- hot path: consume ----------------------------------------
+ * Hashtable::consume_seqfile<FastxReader> (src/oxli/hashtable.cc:125-150):
+ * drains `p`, cleans every read (read_parsers.cc:53-69), counts every k-mer.
+ * Returns this call's share of (reads, k-mers).  mode 1 = consume_seqfile_and_tag
+ * (src/oxli/hashgraph.cc:290-320). */
+int kh_consume_parser(kh_graph *g, kh_parser *p, int mode, uint32_t *reads, uint64_t *kmers);
+/* Hashtable::consume_string over a batch of reads (src/oxli/hashtable.cc:280-294).
+ * seqs = concatenated reads, offsets[nreads+1]; clean != 0 applies
+ * _to_valid_dna first (consume_seqfile semantics), 0 hashes raw (consume()). */
+int kh_consume_seqs(kh_graph *g, const char *seqs, const uint64_t *offsets, uint64_t nreads,
+                    int clean, uint64_t *kmers);
+/* device-resident packed batch (bench / multi-GPU path): `d_words` 2-bit
+ * packed bases (kh_device.h layout) and `d_kmer_off[nreads+1]` k-mer prefix
+ * offsets, both already in this graph's device memory.  Every read must hold
+ * at least one k-mer.  Asynchronous on the graph's stream. */
+int kh_consume_packed_device(kh_graph *g, const uint64_t *d_words, const uint64_t *d_kmer_off,
+                             uint64_t nreads, uint64_t nkmers);
+/* explicit hashes: Hashtable::count/add(HashIntoType) (include/oxli/hashtable.hh:222-243);
+ * is_new[n] (nullable) receives Storage::add's return per hash, in order. */
+int kh_add_hashes(kh_graph *g, const uint64_t *hashes, uint64_t n, uint8_t *is_new);
+
+/* ---------------- queries --------------------------------------------------- */
+/* Storage::get_count per hash (storage.hh:206-219, 362-379, 627-649) */
+int kh_get_counts(kh_graph *g, const uint64_t *hashes, uint64_t n, uint16_t *out);
+/* Hashtable::get_median_count per read (src/oxli/hashtable.cc:299-328); reads
+ * with no k-mer get status[r] = 1 (the reference throws for them). */
+int kh_median_counts(kh_graph *g, const char *seqs, const uint64_t *offsets, uint64_t nreads,
+                     uint16_t *med, float *avg, float *stddev, uint8_t *status);
+/* Hashtable::abundance_distribution (src/oxli/hashtable.cc:451-493);
+ * dist[65536]. */
+int kh_abundance_distribution(kh_graph *g, kh_parser *p, kh_graph *tracking, uint64_t *dist);
+
+/* ---------------- tables, files, tags ---------------------------------------- */
+int kh_graph_table_nbytes(kh_graph *g, int i, uint64_t *out);
+int kh_graph_copy_table(kh_graph *g, int i, uint8_t *dst);      /* get_raw_tables() */
+int kh_graph_save(kh_graph *g, const char *path);               /* storage.cc:99-136,582-803 */
+/* Countgraph/Nodegraph/SmallCountgraph .load (graphs.pyx:302-307);
+ * expected_storage checks the file type code like the reference readers. */
+int kh_graph_load(const char *path, int expected_storage, int hash_kind, int device,
+                  kh_graph **out);
+int kh_graph_n_tags(kh_graph *g, uint64_t *out);
+int kh_graph_get_tags(kh_graph *g, uint64_t *out);              /* ascending */
+int kh_graph_add_tag(kh_graph *g, uint64_t h);
+int kh_graph_save_tagset(kh_graph *g, const char *path);        /* hashgraph.cc:55-88 */
+int kh_graph_load_tagset(kh_graph *g, const char *path, int clear);
+
+/* ---------------- benchmark support -----------------------------------------
+ * seeded synthetic 2-bit reads (khmer_amd/synth.py's definition) generated
+ * straight into HBM: reads r0 .. r0+nreads-1 of length read_len, packed
+ * contiguously (nreads*read_len/32 + 2 words), k-mer offsets r*(read_len-k+1). */
+int kh_synth_packed_device(int device, uint64_t seed, uint64_t r0, uint64_t nreads, int read_len, int k,
+                           uint64_t *d_words, uint64_t *d_kmer_off);
+int kh_device_malloc(int device, uint64_t bytes, void **out);
+int kh_device_free(int device, void *p);
+int kh_device_synchronize(int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

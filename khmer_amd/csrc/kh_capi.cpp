@@ -1,0 +1,764 @@
+// kh_capi.cpp -- the extern "C" boundary of libkhmer_hip.so (include/khmer_hip.h).
+// Every entry point converts exceptions into status codes + a thread-local
+// message (the reference maps C++ exceptions to Python ones,
+// khmer/_oxli/oxli_exception_convert.cc:9-31).
+#include <errno.h>
+#include <limits.h>
+#include <stdio.h>
+#include <string.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <fstream>
+#include <new>
+#include <string>
+
+#include "../../include/khmer_hip.h"
+#include "kh_internal.h"
+
+namespace kh {
+struct Parser;
+Parser *parser_open(const char *path);
+void parser_close(Parser *p);
+int parser_next_read(Parser *p, ReadView *rv);
+uint64_t parser_num_reads(Parser *p);
+bool parser_is_complete(Parser *p);
+void parser_fill_batch(Parser *p, HostBatch &b, int k, uint64_t max_kmers, uint64_t max_bases, bool *done,
+                       uint64_t *taken);
+void engine_hash_batch(Graph *g, const HostBatch &b, uint64_t *h_out);
+void engine_synth_packed(int device, uint64_t seed, uint64_t r0, uint64_t nreads, int L, int k, uint64_t *d_words,
+                         uint64_t *d_koff);
+}  // namespace kh
+
+using namespace kh;
+
+struct kh_graph { Graph *g; };
+struct kh_parser { Parser *p; };
+
+static thread_local std::string tl_err;
+
+template <class F>
+static int guard(F &&f) {
+    try {
+        f();
+        return KH_OK;
+    } catch (const Error &e) {
+        tl_err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        tl_err = "out of memory";
+        return KH_ENOMEM;
+    } catch (const std::exception &e) {
+        tl_err = e.what();
+        return KH_ERUNTIME;
+    }
+}
+
+#define CHECK_PTR(p) do { if (!(p)) fail(KH_EVALUE, "null handle"); } while (0)
+
+extern "C" {
+
+const char *kh_last_error(void) { return tl_err.c_str(); }
+int kh_abi_version(void) { return KH_ABI_VERSION; }
+
+int kh_device_count(int *n) {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return KH_OK;
+}
+
+// ---------------- hashing ---------------------------------------------------
+int kh_hash_twobit(const char *kmer, int k, uint64_t *fwd, uint64_t *rc, uint64_t *canon) {
+    return guard([&] {
+        uint64_t f, r;
+        uint64_t h = hash_twobit(kmer, k, &f, &r);
+        if (fwd) *fwd = f;
+        if (rc) *rc = r;
+        if (canon) *canon = h;
+    });
+}
+
+int kh_reverse_hash(uint64_t h, int k, char *out) {
+    return guard([&] {
+        if (k < 0 || k > 32) fail(KH_EVALUE, "k-mer size must be <= 32");
+        std::string s = revhash(h, k);
+        memcpy(out, s.c_str(), (size_t)k + 1);
+    });
+}
+
+int kh_hash_murmur(const char *kmer, int len, uint64_t *canon, uint64_t *fwd) {
+    return guard([&] {
+        if (canon) *canon = hash_murmur(kmer, len);
+        if (fwd) *fwd = hash_murmur_fwd(kmer, len);
+    });
+}
+
+int kh_reverse_complement(const char *s, size_t len, char *out) {
+    return guard([&] {
+        std::string r = revcomp(s, len);
+        memcpy(out, r.data(), len);
+        out[len] = 0;
+    });
+}
+
+int kh_kmer_hashes(int hash_kind, int k, const char *seq, size_t len, uint64_t *out, uint64_t *n_out) {
+    return guard([&] {
+        std::vector<uint64_t> v;
+        kmer_hashes_host(hash_kind, k, seq, len, v);
+        if (out) memcpy(out, v.data(), v.size() * 8);
+        *n_out = v.size();
+    });
+}
+
+// ---------------- primes -----------------------------------------------------
+int kh_is_prime(uint64_t n, int *out) {
+    return guard([&] { *out = is_prime(n) ? 1 : 0; });
+}
+
+int kh_get_n_primes_near_x(uint32_t n, uint64_t x, uint64_t *out, uint32_t *found) {
+    return guard([&] {
+        std::vector<uint64_t> v = primes_near(n, x);
+        memcpy(out, v.data(), v.size() * 8);
+        *found = (uint32_t)v.size();
+    });
+}
+
+// ---------------- parser ----------------------------------------------------
+int kh_parser_open(const char *path, kh_parser **out) {
+    return guard([&] {
+        Parser *p = parser_open(path);
+        *out = new kh_parser{p};
+    });
+}
+
+int kh_parser_next_read(kh_parser *p, const char **name, size_t *name_len, const char **seq, size_t *seq_len,
+                        const char **qual, size_t *qual_len) {
+    int rc = KH_OK;
+    int st = guard([&] {
+        CHECK_PTR(p);
+        ReadView rv;
+        rc = parser_next_read(p->p, &rv);
+        if (rc != KH_OK) return;
+        *name = rv.name; *name_len = rv.name_len;
+        *seq = rv.seq; *seq_len = rv.seq_len;
+        *qual = rv.qual; *qual_len = rv.qual_len;
+    });
+    return st != KH_OK ? st : rc;
+}
+
+int kh_parser_num_reads(kh_parser *p, uint64_t *out) {
+    return guard([&] { CHECK_PTR(p); *out = parser_num_reads(p->p); });
+}
+
+int kh_parser_is_complete(kh_parser *p, int *out) {
+    return guard([&] { CHECK_PTR(p); *out = parser_is_complete(p->p) ? 1 : 0; });
+}
+
+void kh_parser_close(kh_parser *p) {
+    if (!p) return;
+    parser_close(p->p);
+    delete p;
+}
+
+// ---------------- graph lifecycle -----------------------------------------------
+int kh_graph_create(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables, int device,
+                    kh_graph **out) {
+    return guard([&] {
+        Graph *g = graph_create(storage, hash_kind, k, sizes, n_tables, device);
+        *out = new kh_graph{g};
+    });
+}
+
+void kh_graph_destroy(kh_graph *g) {
+    if (!g) return;
+    delete g->g;
+    delete g;
+}
+
+int kh_graph_info(kh_graph *h, int *storage, int *hash_kind, int *k, int *n_tables) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        if (storage) *storage = g->kind;
+        if (hash_kind) *hash_kind = g->hash;
+        if (k) *k = g->k;
+        if (n_tables) *n_tables = g->n;
+    });
+}
+
+int kh_graph_tablesizes(kh_graph *h, uint64_t *out) {
+    return guard([&] {
+        CHECK_PTR(h);
+        memcpy(out, h->g->sizes.data(), h->g->sizes.size() * 8);
+    });
+}
+
+int kh_graph_set_use_bigcount(kh_graph *h, int on) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        // Storage::set_use_bigcount (src/oxli/storage.cc:50-56)
+        if (g->kind != BYTE) fail(KH_EVALUE, "bigcount is not supported for this storage.");
+        g->use_bigcount = on != 0;
+        g->prm.use_bigcount = on ? 1 : 0;
+    });
+}
+
+int kh_graph_get_use_bigcount(kh_graph *h, int *on) {
+    return guard([&] { CHECK_PTR(h); *on = h->g->use_bigcount ? 1 : 0; });
+}
+
+int kh_graph_n_unique_kmers(kh_graph *h, uint64_t *out) {
+    return guard([&] { CHECK_PTR(h); *out = h->g->n_unique; });
+}
+
+int kh_graph_n_occupied(kh_graph *h, uint64_t *out) {
+    return guard([&] { CHECK_PTR(h); *out = h->g->n_occupied; });
+}
+
+int kh_graph_set_batch_kmers(kh_graph *h, uint64_t max_kmers) {
+    return guard([&] {
+        CHECK_PTR(h);
+        if (max_kmers < 1024 || max_kmers > (1ull << 31)) fail(KH_EVALUE, "batch size out of range");
+        h->g->batch_kmers = max_kmers;
+    });
+}
+
+}  // extern "C"
+
+// ---------------- consume helpers -------------------------------------------------
+// Hashgraph::consume_sequence_and_tag state machine (src/oxli/hashgraph.cc:200-271)
+// over one batch: is-new flags and hashes come from the device pass.
+static uint64_t tag_batch(Graph *g, const HostBatch &b, const uint8_t *isnew, const uint64_t *hashes) {
+    const uint32_t density = 40;  // DEFAULT_TAG_DENSITY, include/oxli/oxli.hh:83
+    uint64_t consumed = 0;
+    for (uint64_t r = 0; r < b.nreads(); r++) {
+        const uint64_t a = b.koff[r], e = b.koff[r + 1];
+        uint32_t since = density / 2 + 1;
+        uint64_t kmer = 0;
+        for (uint64_t j = a; j < e; j++) {
+            kmer = hashes[j];
+            const bool nw = isnew[j] != 0;
+            if (nw) {
+                ++consumed;
+                ++since;
+            } else if (g->tags.count(kmer)) {
+                since = 1;
+            } else {
+                ++since;
+            }
+            if (since >= density) {
+                g->tags.insert(kmer);
+                since = 1;
+            }
+        }
+        // every packed read holds >= 1 k-mer; the reference also tags the
+        // (uninitialised) k-mer of reads shorter than k -- not reproduced
+        if (since >= density / 2 - 1) g->tags.insert(kmer);
+    }
+    return consumed;
+}
+
+static void consume_batch(Graph *g, const HostBatch &b, int mode, uint64_t *consumed) {
+    if (b.nkmers() == 0) return;
+    if (mode == 0) {
+        engine_consume_host(g, b, nullptr);
+        *consumed += b.nkmers();
+        return;
+    }
+    std::vector<uint8_t> isnew(b.nkmers());
+    std::vector<uint64_t> hashes(b.nkmers());
+    PassOut out{isnew.data(), hashes.data()};
+    engine_consume_host(g, b, &out);
+    *consumed += tag_batch(g, b, isnew.data(), hashes.data());
+}
+
+static uint64_t batch_bases_cap(Graph *g) { return g->batch_kmers * 2 + (1u << 20); }
+
+extern "C" {
+
+int kh_consume_parser(kh_graph *h, kh_parser *ph, int mode, uint32_t *reads, uint64_t *kmers) {
+    *reads = 0;
+    *kmers = 0;
+    return guard([&] {
+        CHECK_PTR(h);
+        CHECK_PTR(ph);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        HostBatch b;
+        b.hash = g->hash;
+        bool done = false;
+        uint64_t consumed = 0, nreads = 0;
+        while (!done) {
+            b.clear();
+            try {
+                parser_fill_batch(ph->p, b, g->k, g->batch_kmers, batch_bases_cap(g), &done, &nreads);
+            } catch (...) {
+                // the reference consumed every read before the bad one, then throws
+                consume_batch(g, b, mode, &consumed);
+                *reads = (uint32_t)nreads;
+                *kmers = consumed;
+                throw;
+            }
+            consume_batch(g, b, mode, &consumed);
+        }
+        *reads = (uint32_t)nreads;
+        *kmers = consumed;
+    });
+}
+
+int kh_consume_seqs(kh_graph *h, const char *seqs, const uint64_t *offsets, uint64_t nreads, int clean,
+                    uint64_t *kmers) {
+    *kmers = 0;
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        HostBatch b;
+        b.hash = g->hash;
+        uint64_t consumed = 0;
+        for (uint64_t r = 0; r < nreads; r++) {
+            const char *s = seqs + offsets[r];
+            // KmerIterator length = strlen (kmer_hash.cc:290)
+            size_t len = strnlen(s, (size_t)(offsets[r + 1] - offsets[r]));
+            if (len >= (size_t)g->k) b.append(s, len, g->k, clean != 0);
+            if (b.nkmers() >= g->batch_kmers) {
+                consume_batch(g, b, 0, &consumed);
+                b.clear();
+            }
+        }
+        consume_batch(g, b, 0, &consumed);
+        *kmers = consumed;
+    });
+}
+
+int kh_consume_packed_device(kh_graph *h, const uint64_t *d_words, const uint64_t *d_kmer_off, uint64_t nreads,
+                             uint64_t nkmers) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        if (g->hash != TWOBIT) fail(KH_EVALUE, "packed 2-bit input requires a 2-bit hashing graph");
+        engine_consume_twobit(g, d_words, d_kmer_off, nreads, nkmers, nullptr);
+    });
+}
+
+int kh_add_hashes(kh_graph *h, const uint64_t *hashes, uint64_t n, uint8_t *is_new) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        if (!n) return;
+        uint64_t *d = nullptr;
+        KH_HIP(hipMalloc((void **)&d, n * 8));
+        KH_HIP(hipMemcpy(d, hashes, n * 8, hipMemcpyHostToDevice));
+        PassOut out{is_new, nullptr};
+        try {
+            engine_consume_hashes(g, d, n, is_new ? &out : nullptr);
+        } catch (...) {
+            (void)hipFree(d);
+            throw;
+        }
+        KH_HIP(hipFree(d));
+    });
+}
+
+int kh_get_counts(kh_graph *h, const uint64_t *hashes, uint64_t n, uint16_t *out) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        engine_get_counts(g, hashes, n, out);
+    });
+}
+
+int kh_median_counts(kh_graph *h, const char *seqs, const uint64_t *offsets, uint64_t nreads, uint16_t *med,
+                     float *avg, float *stddev, uint8_t *status) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        HostBatch b;
+        b.hash = g->hash;
+        std::vector<uint64_t> idx;
+        for (uint64_t r = 0; r < nreads; r++) {
+            const char *s = seqs + offsets[r];
+            size_t len = strnlen(s, (size_t)(offsets[r + 1] - offsets[r]));
+            if (len >= (size_t)g->k) {
+                b.append(s, len, g->k, false);
+                idx.push_back(r);
+                status[r] = 0;
+            } else {
+                status[r] = 1;
+                med[r] = 0;
+                avg[r] = 0;
+                stddev[r] = 0;
+            }
+        }
+        std::vector<uint16_t> m(idx.size());
+        std::vector<float> a(idx.size()), s(idx.size());
+        engine_median(g, b, m.data(), a.data(), s.data());
+        for (size_t t = 0; t < idx.size(); t++) {
+            med[idx[t]] = m[t];
+            avg[idx[t]] = a[t];
+            stddev[idx[t]] = s[t];
+        }
+    });
+}
+
+int kh_abundance_distribution(kh_graph *h, kh_parser *ph, kh_graph *th, uint64_t *dist) {
+    return guard([&] {
+        CHECK_PTR(h);
+        CHECK_PTR(ph);
+        CHECK_PTR(th);
+        Graph *g = h->g, *t = th->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        std::lock_guard<std::recursive_mutex> lk2(t->mu);
+        KH_HIP(hipSetDevice(g->device));
+        if (t->device != g->device) fail(KH_EVALUE, "tracking table must live on the same device");
+        memset(dist, 0, 65536 * sizeof(uint64_t));
+        HostBatch b;
+        b.hash = g->hash;
+        bool done = false;
+        while (!done) {
+            b.clear();
+            uint64_t taken = 0;
+            parser_fill_batch(ph->p, b, g->k, g->batch_kmers, batch_bases_cap(g), &done, &taken);
+            const uint64_t nk = b.nkmers();
+            if (!nk) continue;
+            // self's iterator hashes (hashtable.cc:476-480), tracked in stream order
+            std::vector<uint64_t> hs(nk);
+            engine_hash_batch(g, b, hs.data());
+            std::vector<uint8_t> isnew(nk);
+            uint64_t *d = nullptr;
+            KH_HIP(hipMalloc((void **)&d, nk * 8));
+            KH_HIP(hipMemcpy(d, hs.data(), nk * 8, hipMemcpyHostToDevice));
+            PassOut out{isnew.data(), nullptr};
+            engine_consume_hashes(t, d, nk, &out);
+            KH_HIP(hipFree(d));
+            std::vector<uint64_t> sel;
+            for (uint64_t j = 0; j < nk; j++)
+                if (isnew[j]) sel.push_back(hs[j]);
+            std::vector<uint16_t> cnt(sel.size());
+            engine_get_counts(g, sel.data(), sel.size(), cnt.data());
+            for (uint16_t c : cnt) dist[c]++;
+        }
+    });
+}
+
+// ---------------- tables & files ------------------------------------------------
+int kh_graph_table_nbytes(kh_graph *h, int i, uint64_t *out) {
+    return guard([&] {
+        CHECK_PTR(h);
+        if (i < 0 || i >= h->g->n) fail(KH_EVALUE, "table index out of range");
+        *out = h->g->nbytes[(size_t)i];
+    });
+}
+
+int kh_graph_copy_table(kh_graph *h, int i, uint8_t *dst) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        if (i < 0 || i >= g->n) fail(KH_EVALUE, "table index out of range");
+        KH_HIP(hipSetDevice(g->device));
+        engine_download_table(g, i, dst);
+    });
+}
+
+}  // extern "C"
+
+// writer abstraction: plain or gzip (ByteStorageFile::save picks by extension,
+// src/oxli/storage.cc:255-269).  The gzip writer advances through the table
+// (the reference re-writes the table head for tables > INT_MAX bytes, F7).
+struct Out {
+    FILE *f = nullptr;
+    gzFile gz = nullptr;
+    void write(const void *p, size_t n) {
+        const char *c = (const char *)p;
+        while (n) {
+            size_t chunk = std::min<size_t>(n, (size_t)INT_MAX / 2);
+            if (gz) {
+                if (gzwrite(gz, c, (unsigned)chunk) == 0) fail(KH_EFILE, "gzwrite failed while writing counting hash");
+            } else if (fwrite(c, 1, chunk, f) != chunk) {
+                fail(KH_EFILE, strerror(errno));
+            }
+            c += chunk;
+            n -= chunk;
+        }
+    }
+    void close() {
+        if (gz) { gzclose(gz); gz = nullptr; }
+        if (f) {
+            if (fclose(f) != 0) { f = nullptr; fail(KH_EFILE, strerror(errno)); }
+            f = nullptr;
+        }
+    }
+    ~Out() {
+        if (gz) gzclose(gz);
+        if (f) fclose(f);
+    }
+};
+
+static bool ends_with_gz(const std::string &s) {
+    size_t dot = s.find_last_of('.');
+    return dot != std::string::npos && s.substr(dot + 1) == "gz";
+}
+
+extern "C" int kh_graph_save(kh_graph *h, const char *path) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        Out o;
+        const bool gz = g->kind == BYTE && ends_with_gz(path);
+        if (gz) {
+            o.gz = gzopen(path, "wb");
+            if (!o.gz) fail(KH_EFILE, strerror(errno));
+        } else {
+            o.f = fopen(path, "wb");
+            if (!o.f) fail(KH_EFILE, strerror(errno));
+        }
+        // header: doc/dev/binary-file-formats.rst; storage.cc:99-136 (bit),
+        // 582-638 (byte), 772-803 (nibble)
+        o.write("OXLI", 4);
+        unsigned char version = 4, type = (unsigned char)g->kind;
+        o.write(&version, 1);
+        o.write(&type, 1);
+        if (g->kind == BYTE) {
+            unsigned char bc = g->use_bigcount ? 1 : 0;
+            o.write(&bc, 1);
+        }
+        uint32_t k = (uint32_t)g->k;
+        unsigned char n = (unsigned char)g->n;
+        uint64_t occ = g->n_occupied;
+        o.write(&k, 4);
+        o.write(&n, 1);
+        o.write(&occ, 8);
+        std::vector<uint8_t> buf;
+        for (int i = 0; i < g->n; i++) {
+            uint64_t sz = g->sizes[(size_t)i];
+            o.write(&sz, 8);
+            buf.resize(g->nbytes[(size_t)i]);
+            engine_download_table(g, i, buf.data());
+            o.write(buf.data(), buf.size());
+        }
+        if (g->kind == BYTE) {
+            std::vector<std::pair<uint64_t, uint16_t>> v(g->bigcounts.begin(), g->bigcounts.end());
+            std::sort(v.begin(), v.end());
+            uint64_t nb = v.size();
+            o.write(&nb, 8);
+            for (auto &kv : v) {
+                o.write(&kv.first, 8);
+                o.write(&kv.second, 2);
+            }
+        }
+        o.close();
+    });
+}
+
+// reader: plain or gzip (ByteStorageGzFileReader for *.gz countgraphs)
+struct In {
+    gzFile gz = nullptr;
+    std::string path;
+    void read(void *p, size_t n) {
+        char *c = (char *)p;
+        while (n) {
+            unsigned chunk = (unsigned)std::min<size_t>(n, (size_t)INT_MAX / 2);
+            int got = gzread(gz, c, chunk);
+            if (got <= 0) fail(KH_EFILE, "Unexpected end of k-mer graph file: " + path);
+            c += got;
+            n -= (size_t)got;
+        }
+    }
+    ~In() { if (gz) gzclose(gz); }
+};
+
+extern "C" int kh_graph_load(const char *path, int expected_storage, int hash_kind, int device, kh_graph **out) {
+    return guard([&] {
+        In in;
+        in.path = path;
+        in.gz = gzopen(path, "rb");
+        if (!in.gz) fail(KH_EFILE, std::string("Cannot open k-mer graph file: ") + path);
+        char sig[4];
+        unsigned char version = 0, type = 0;
+        in.read(sig, 4);
+        in.read(&version, 1);
+        in.read(&type, 1);
+        if (memcmp(sig, "OXLI", 4) != 0) {
+            char msg[128];
+            snprintf(msg, sizeof msg, "Does not start with signature for a oxli file: 0x%x%x%x%x Should be: OXLI",
+                     (unsigned char)sig[0], (unsigned char)sig[1], (unsigned char)sig[2], (unsigned char)sig[3]);
+            fail(KH_EFILE, msg);
+        }
+        if (version != 4)
+            fail(KH_EFILE, "Incorrect file format version " + std::to_string(version) + " while reading k-mer graph from " +
+                               path + "; should be 4");
+        if (type != (unsigned char)expected_storage)
+            fail(KH_EFILE, "Incorrect file format type " + std::to_string(type) + " while reading k-mer graph from " + path);
+        unsigned char bc = 0;
+        if (type == BYTE) in.read(&bc, 1);
+        uint32_t k = 0;
+        unsigned char n = 0;
+        uint64_t occ = 0;
+        in.read(&k, 4);
+        in.read(&n, 1);
+        in.read(&occ, 8);
+        if (n < 1) fail(KH_EFILE, std::string("Unexpected end of k-mer graph file: ") + path);
+        std::vector<uint64_t> sizes;
+        std::vector<std::vector<uint8_t>> tabs;
+        for (int i = 0; i < n; i++) {
+            uint64_t sz = 0;
+            in.read(&sz, 8);
+            uint64_t nb = type == BIT ? sz / 8 + 1 : type == NIBBLE ? sz / 2 + 1 : sz;
+            sizes.push_back(sz);
+            tabs.emplace_back(nb);
+            in.read(tabs.back().data(), nb);
+        }
+        std::vector<std::pair<uint64_t, uint16_t>> bcs;
+        if (type == BYTE) {
+            uint64_t nbig = 0;
+            in.read(&nbig, 8);
+            for (uint64_t t = 0; t < nbig; t++) {
+                uint64_t key;
+                uint16_t val;
+                in.read(&key, 8);
+                in.read(&val, 2);
+                bcs.emplace_back(key, val);
+            }
+        }
+        int kk = (int)k;
+        if (hash_kind == TWOBIT && kk > 32) fail(KH_EFILE, "k-mer size in file exceeds 32");
+        Graph *g = graph_create(type, hash_kind, kk, sizes.data(), n, device);
+        try {
+            for (int i = 0; i < n; i++) engine_upload_table(g, i, tabs[(size_t)i].data());
+            g->n_occupied = occ;
+            g->n_unique = 0;  // not stored in the file (storage.hh:143-165)
+            g->use_bigcount = bc != 0;
+            g->prm.use_bigcount = bc ? 1 : 0;
+            for (auto &kv : bcs) g->bigcounts[kv.first] = kv.second;
+            g->bc_dirty = true;
+        } catch (...) {
+            delete g;
+            throw;
+        }
+        *out = new kh_graph{g};
+    });
+}
+
+// ---------------- tags ------------------------------------------------------------
+extern "C" {
+
+int kh_graph_n_tags(kh_graph *h, uint64_t *out) {
+    return guard([&] { CHECK_PTR(h); *out = h->g->tags.size(); });
+}
+
+int kh_graph_get_tags(kh_graph *h, uint64_t *out) {
+    return guard([&] {
+        CHECK_PTR(h);
+        std::vector<uint64_t> v(h->g->tags.begin(), h->g->tags.end());
+        std::sort(v.begin(), v.end());
+        memcpy(out, v.data(), v.size() * 8);
+    });
+}
+
+int kh_graph_add_tag(kh_graph *h, uint64_t t) {
+    return guard([&] { CHECK_PTR(h); h->g->tags.insert(t); });
+}
+
+// Hashgraph::save_tagset (src/oxli/hashgraph.cc:55-88); std::set order = ascending
+int kh_graph_save_tagset(kh_graph *h, const char *path) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::vector<uint64_t> v(g->tags.begin(), g->tags.end());
+        std::sort(v.begin(), v.end());
+        Out o;
+        o.f = fopen(path, "wb");
+        if (!o.f) fail(KH_EFILE, strerror(errno));
+        o.write("OXLI", 4);
+        unsigned char version = 4, type = 3;  // SAVED_TAGS
+        o.write(&version, 1);
+        o.write(&type, 1);
+        uint32_t k = (uint32_t)g->k;
+        uint64_t n = v.size();
+        uint32_t density = 40;
+        o.write(&k, 4);
+        o.write(&n, 8);
+        o.write(&density, 4);
+        o.write(v.data(), n * 8);
+        o.close();
+    });
+}
+
+// Hashgraph::load_tagset (src/oxli/hashgraph.cc:90-152)
+int kh_graph_load_tagset(kh_graph *h, const char *path, int clear) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        In in;
+        in.path = path;
+        in.gz = gzopen(path, "rb");
+        if (!in.gz) fail(KH_EFILE, std::string("Cannot open tagset file: ") + path);
+        char sig[4];
+        unsigned char version = 0, type = 0;
+        in.read(sig, 4);
+        in.read(&version, 1);
+        in.read(&type, 1);
+        if (memcmp(sig, "OXLI", 4) != 0) fail(KH_EFILE, "Does not start with signature for a oxli file");
+        if (version != 4) fail(KH_EFILE, "Incorrect file format version " + std::to_string(version) +
+                                             " while reading tagset from " + path + "; should be 4");
+        if (type != 3) fail(KH_EFILE, "Incorrect file format type " + std::to_string(type) + " while reading tagset from " + path);
+        uint32_t k = 0, density = 0;
+        uint64_t n = 0;
+        in.read(&k, 4);
+        in.read(&n, 8);
+        in.read(&density, 4);
+        if ((int)k != g->k) fail(KH_EFILE, "Incorrect k-mer size in tagset file");
+        std::vector<uint64_t> v(n);
+        in.read(v.data(), n * 8);
+        if (clear) g->tags.clear();
+        g->tags.insert(v.begin(), v.end());
+    });
+}
+
+}  // extern "C"
+
+// ---------------- benchmark support -------------------------------------------------
+extern "C" int kh_synth_packed_device(int device, uint64_t seed, uint64_t r0, uint64_t nreads, int read_len, int k,
+                                      uint64_t *d_words, uint64_t *d_kmer_off) {
+    return guard([&] {
+        if (read_len < k || k < 1 || k > 32) fail(KH_EVALUE, "need 1 <= k <= read length and k <= 32");
+        engine_synth_packed(device, seed, r0, nreads, read_len, k, d_words, d_kmer_off);
+    });
+}
+
+extern "C" int kh_device_malloc(int device, uint64_t bytes, void **out) {
+    return guard([&] {
+        KH_HIP(hipSetDevice(device));
+        KH_HIP(hipMalloc(out, bytes));
+    });
+}
+
+extern "C" int kh_device_free(int device, void *p) {
+    return guard([&] {
+        KH_HIP(hipSetDevice(device));
+        KH_HIP(hipFree(p));
+    });
+}
+
+extern "C" int kh_device_synchronize(int device) {
+    return guard([&] {
+        KH_HIP(hipSetDevice(device));
+        KH_HIP(hipDeviceSynchronize());
+    });
+}

@@ -1,0 +1,146 @@
+// kh_host.cpp -- host-side helpers of libkhmer_hip.so: scalar hashing
+// utilities (the khmer._khmer module functions), primes, read packing.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "kh_internal.h"
+
+namespace kh {
+
+// twobit_repr (include/oxli/kmer_hash.hh:69-73): A=0 T=1 C=2 else 3
+static inline uint64_t repr(unsigned char c) { return c == 'A' ? 0 : c == 'T' ? 1 : c == 'C' ? 2 : 3; }
+
+// _hash (src/oxli/kmer_hash.cc:65-95)
+uint64_t hash_twobit(const char *kmer, int k, uint64_t *f, uint64_t *r) {
+    if (k > 32) fail(1, "Supplied kmer string doesn't match the underlying k-size.");
+    if ((int)strnlen(kmer, (size_t)k) < k) fail(1, "k-mer is too short to hash.");
+    uint64_t h = 0;
+    for (int i = 0; i < k; i++) h = (h << 2) | repr((unsigned char)kmer[i]);
+    uint64_t rc = revcomp2(h, k);
+    if (f) *f = h;
+    if (r) *r = rc;
+    return h < rc ? h : rc;
+}
+
+// _revhash (src/oxli/kmer_hash.cc:134-150)
+std::string revhash(uint64_t h, int k) {
+    std::string s((size_t)k, 'A');
+    static const char sym[4] = {'A', 'T', 'C', 'G'};
+    for (int i = k - 1; i >= 0; i--) { s[(size_t)i] = sym[h & 3]; h >>= 2; }
+    return s;
+}
+
+// _revcomp (src/oxli/kmer_hash.cc:152-166)
+std::string revcomp(const char *s, size_t len) {
+    std::string out(len, ' ');
+    for (size_t i = 0; i < len; i++) out[len - 1 - i] = iupac_comp((uint8_t)s[i]);
+    return out;
+}
+
+// _hash_murmur / _hash_murmur_forward (src/oxli/kmer_hash.cc:177-207)
+uint64_t hash_murmur(const char *kmer, int k) { return murmur_canonical((const uint8_t *)kmer, k); }
+uint64_t hash_murmur_fwd(const char *kmer, int k) {
+    const uint8_t *s = (const uint8_t *)kmer;
+    return murmur3_x64_128_h1([&](int i) { return s[i]; }, k);
+}
+
+// is_prime / get_n_primes_near_x (include/oxli/hashtable.hh:79-123)
+bool is_prime(uint64_t n) {
+    if (n < 2) return false;
+    if (n == 2) return true;
+    if (n % 2 == 0) return false;
+    for (unsigned long long i = 3; i < sqrt((double)n) + 1; i += 2)
+        if (n % i == 0) return false;
+    return true;
+}
+
+std::vector<uint64_t> primes_near(uint32_t n, uint64_t x) {
+    std::vector<uint64_t> out;
+    if (x == 1) { out.push_back(1); return out; }
+    uint64_t i = x - 1;
+    if (i % 2 == 0) i--;
+    while (out.size() != n) {
+        if (is_prime(i)) out.push_back(i);
+        if (i == 1) break;
+        i -= 2;
+    }
+    return out;
+}
+
+// k-mer hash iteration over one string (KmerIterator, src/oxli/kmer_hash.cc:278-343;
+// MurmurKmerHashIterator, include/oxli/hashtable.hh:436-491); length = strlen.
+void kmer_hashes_host(int hash_kind, int k, const char *seq, size_t len, std::vector<uint64_t> &out) {
+    size_t slen = strnlen(seq, len);
+    if (slen < (size_t)k || k < 1) return;
+    if (hash_kind == MURMUR) {
+        for (size_t i = 0; i + (size_t)k <= slen; i++) out.push_back(hash_murmur(seq + i, k));
+        return;
+    }
+    if (k > 32) fail(1, "Supplied kmer string doesn't match the underlying k-size.");
+    uint64_t mask = kmer_mask(k), f = 0;
+    for (size_t i = 0; i < slen; i++) {
+        f = ((f << 2) | repr((unsigned char)seq[i])) & mask;
+        if (i + 1 >= (size_t)k) out.push_back(canonical2(f, k));
+    }
+}
+
+// ---- byte maps -------------------------------------------------------------
+struct Maps {
+    uint8_t clean2[256], raw2[256], cleanc[256];
+    Maps() {
+        for (int c = 0; c < 256; c++) {
+            raw2[c] = (uint8_t)repr((unsigned char)c);
+            // _to_valid_dna (src/oxli/read_parsers.cc:53-69): ACGT/acgt kept
+            // (upper-cased), everything else becomes 'A'
+            char cc;
+            switch (c) {
+            case 'A': case 'C': case 'G': case 'T': cc = (char)c; break;
+            case 'a': case 'c': case 'g': case 't': cc = (char)(c - 32); break;
+            default: cc = 'A';
+            }
+            cleanc[c] = (uint8_t)cc;
+            clean2[c] = (uint8_t)repr((unsigned char)cc);
+        }
+    }
+};
+static const Maps g_maps;
+
+void HostBatch::append(const char *s, size_t len, int k, bool clean) {
+    uint64_t nk = len - (uint64_t)k + 1;
+    if (hash == MURMUR) {
+        const uint8_t *mp = clean ? g_maps.cleanc : nullptr;
+        size_t off = bytes.size();
+        bytes.resize(off + len);
+        if (mp) for (size_t i = 0; i < len; i++) bytes[off + i] = mp[(uint8_t)s[i]];
+        else memcpy(bytes.data() + off, s, len);
+    } else {
+        const uint8_t *mp = clean ? g_maps.clean2 : g_maps.raw2;
+        uint64_t need_words = (nbases + len + 31) / 32 + 1;  // +1 padding word
+        if (words.size() < need_words) words.resize(std::max<size_t>(need_words, words.size() * 3 / 2 + 1), 0);
+        uint64_t p = nbases;
+        size_t i = 0;
+        // head: fill the partial word
+        while (i < len && (p & 31)) {
+            words[p >> 5] |= (uint64_t)mp[(uint8_t)s[i]] << (62 - 2 * (p & 31));
+            i++; p++;
+        }
+        // body: 32 bases per word
+        while (i + 32 <= len) {
+            uint64_t w = 0;
+            for (int b = 0; b < 32; b++) w = (w << 2) | mp[(uint8_t)s[i + b]];
+            words[p >> 5] = w;
+            i += 32; p += 32;
+        }
+        while (i < len) {
+            words[p >> 5] |= (uint64_t)mp[(uint8_t)s[i]] << (62 - 2 * (p & 31));
+            i++; p++;
+        }
+    }
+    nbases += len;
+    koff.push_back(koff.back() + nk);
+    read_kmers.push_back((uint32_t)nk);
+}
+
+}  // namespace kh

@@ -1,0 +1,172 @@
+// kh_internal.h -- internal structures of libkhmer_hip.so (not part of the ABI).
+#pragma once
+#include <stdint.h>
+
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "kh_device.h"
+#include "../../include/khmer_hip.h"
+
+namespace kh {
+
+// ---- errors: mapped to status codes at the C-ABI edge (kh_capi.cpp) ----
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+[[noreturn]] inline void fail(int code, const std::string &msg) { throw Error(code, msg); }
+
+#define KH_HIP(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) {                                                             \
+            if (e_ == hipErrorOutOfMemory)                                                  \
+                ::kh::fail(4, std::string("device out of memory: ") + #expr);               \
+            ::kh::fail(5, std::string("HIP error ") + hipGetErrorString(e_) + " at " + #expr); \
+        }                                                                                   \
+    } while (0)
+
+constexpr int MAXT = 32;  // tables per graph on device (NibbleStorage's own cap, storage.hh:290)
+
+// ---- partition geometry -----------------------------------------------------
+// Every table bin gets a global id G = tbase[i] + bin.  Regions are 2^s0 bins
+// (one LDS-resident workgroup each); level-1 buckets are 2^(s0+s2) bins; each
+// table starts on a bucket boundary.
+struct Geometry {
+    int s0 = 14;          // log2 region bins
+    int s2 = 10;          // log2 regions per level-1 bucket
+    uint32_t F1 = 1;      // level-1 buckets
+    uint64_t tbase[MAXT];
+    uint32_t bucket_table[8192];
+};
+
+// kernel parameter block (passed by value)
+struct Params {
+    int kind, hash, k, n;
+    int s0, s2;
+    uint32_t F1;
+    int use_bigcount;
+    uint64_t p[MAXT];         // table sizes (bins)
+    uint64_t m[MAXT];         // Barrett constants
+    uint64_t tbase[MAXT];     // global bin base of table i
+    uint64_t tbyte[MAXT];     // byte offset of table i in the table arena
+    uint64_t tbytes[MAXT];    // storage bytes of table i
+};
+
+// device workspace of one pipeline pass (grown on demand)
+struct Workspace {
+    uint64_t cap_kmers = 0, cap_recs = 0;
+    uint32_t *rec1_off = nullptr, *rec1_j = nullptr;
+    uint32_t *rec2_off = nullptr, *rec2_j = nullptr;
+    uint8_t *newf = nullptr, *fullf = nullptr;   // per k-mer flags
+    uint64_t *bc = nullptr;                      // bigcount candidate hashes
+    uint64_t *hashes_out = nullptr;              // optional per-k-mer hashes
+    // bucket bookkeeping
+    uint32_t *cnt1 = nullptr;        // [F1]
+    uint64_t *off1 = nullptr;        // [F1+1]
+    uint64_t *cur1 = nullptr;        // [F1]
+    uint32_t *tile1 = nullptr;       // [F1+1] tile prefix of level-2 passes
+    uint32_t *cnt2 = nullptr;        // [F1*2^s2]
+    uint64_t *off2 = nullptr;        // [F1*2^s2 + 1]
+    uint64_t *cur2 = nullptr;        // [F1*2^s2]
+    uint64_t *cross = nullptr;       // crossing bins: (global bin << 8) | c0
+    uint64_t *ctr = nullptr;         // counters, see CTR_*
+    uint64_t *h_ctr = nullptr;       // pinned host mirror
+    uint64_t cap_regions = 0, cap_cross = 0, cap_bc = 0;
+    // staging for host-fed batches
+    uint64_t *d_words = nullptr, *d_koff = nullptr;
+    uint8_t *d_bytes = nullptr;
+    uint64_t cap_words = 0, cap_koff = 0, cap_bytes = 0;
+};
+enum { CTR_OCC = 0, CTR_UNIQUE, CTR_NCROSS, CTR_NBC, CTR_ERR, CTR_N };
+
+struct Graph {
+    int kind = BYTE, hash = TWOBIT, k = 0, n = 0, device = 0;
+    std::vector<uint64_t> sizes, nbytes;
+    Geometry geo;
+    Params prm;
+    uint8_t *d_tab = nullptr;         // table arena
+    uint64_t arena_bytes = 0;
+    hipStream_t stream = nullptr;
+    uint64_t n_unique = 0, n_occupied = 0;
+    bool use_bigcount = false;
+    std::unordered_map<uint64_t, uint16_t> bigcounts;   // storage.hh:498 KmerCountMap
+    // device mirror of bigcounts for queries (sorted keys / values)
+    uint64_t *d_bc_keys = nullptr;
+    uint16_t *d_bc_vals = nullptr;
+    uint64_t d_bc_n = 0, d_bc_cap = 0;
+    bool bc_dirty = true;
+    std::unordered_set<uint64_t> tags;                  // hashgraph.hh:113 all_tags
+    uint64_t batch_kmers = 1ull << 27;
+    Workspace ws;
+    std::recursive_mutex mu;
+    ~Graph();
+};
+
+// ---- host helpers (kh_host.cpp) ----
+uint64_t hash_twobit(const char *kmer, int k, uint64_t *f, uint64_t *r);
+uint64_t hash_murmur(const char *kmer, int k);
+uint64_t hash_murmur_fwd(const char *kmer, int k);
+std::string revhash(uint64_t h, int k);
+std::string revcomp(const char *s, size_t len);
+bool is_prime(uint64_t n);
+std::vector<uint64_t> primes_near(uint32_t n, uint64_t x);
+void kmer_hashes_host(int hash_kind, int k, const char *seq, size_t len, std::vector<uint64_t> &out);
+
+// host-side batch of reads ready for the device
+struct HostBatch {
+    int hash = TWOBIT;
+    std::vector<uint64_t> words;     // 2-bit packed (TWOBIT)
+    std::vector<uint8_t> bytes;      // ASCII (MURMUR)
+    std::vector<uint64_t> koff{0};   // k-mer prefix offsets per packed read
+    std::vector<uint32_t> read_kmers;  // per packed read
+    uint64_t nbases = 0;
+    uint64_t nkmers() const { return koff.back(); }
+    uint64_t nreads() const { return koff.size() - 1; }
+    void clear() {
+        words.clear(); bytes.clear(); koff.assign(1, 0); read_kmers.clear(); nbases = 0;
+    }
+    // append a read (reads shorter than k are skipped by the caller)
+    void append(const char *s, size_t len, int k, bool clean);
+};
+
+// ---- parser (kh_parser.cpp) ----
+struct Parser;
+struct ReadView {
+    const char *name; size_t name_len;
+    const char *seq; size_t seq_len;
+    const char *qual; size_t qual_len;
+};
+
+// ---- engine (kh_engine.hip) ----
+Graph *graph_create(int kind, int hash, int k, const uint64_t *sizes, int n, int device);
+void graph_zero_counters(Graph *g);
+void graph_prepare_params(Graph *g);
+// run one device pipeline pass over a device-resident batch.
+// Optional outputs: per-k-mer is-new flags and hashes (device pointers filled
+// into ws; copied to host by the caller).
+struct PassOut {
+    uint8_t *h_new = nullptr;     // host [nkmers]
+    uint64_t *h_hash = nullptr;   // host [nkmers]
+};
+void engine_consume_twobit(Graph *g, const uint64_t *d_words, const uint64_t *d_koff,
+                           uint64_t nreads, uint64_t nkmers, const PassOut *out);
+void engine_consume_bytes(Graph *g, const uint8_t *d_bytes, const uint64_t *d_koff,
+                          uint64_t nreads, uint64_t nkmers, const PassOut *out);
+void engine_consume_hashes(Graph *g, const uint64_t *d_hashes, uint64_t n, const PassOut *out);
+void engine_consume_host(Graph *g, const HostBatch &b, const PassOut *out);
+void engine_get_counts(Graph *g, const uint64_t *h_hashes, uint64_t n, uint16_t *out);
+void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, float *sd);
+void engine_sync_bigcounts(Graph *g);
+void engine_download_table(Graph *g, int i, uint8_t *dst);
+void engine_upload_table(Graph *g, int i, const uint8_t *src);
+
+}  // namespace kh
