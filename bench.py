@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""bench.py -- k-mers hashed/s into a Countgraph on MI355X (BASELINE.json).
+
+Workload (BASELINE.json configs[1]): Countgraph k=21,
+4 tables of the largest primes < 1e9 (4.0 GB of 8-bit counters, bigcount on as
+in load-into-counting.py), 50M synthetic 150 bp reads per GPU (6.5e9 k-mers).
+The reads are generated straight into HBM before timing
+(kh_synth_packed_device = khmer_amd.synth's seeded stream).  One step = reset
+the tables, then consume every read (hash -> partition -> LDS apply ->
+finalize), i.e. the whole hot path over the whole batch.
+
+Multi-GPU (torchrun, one rank per GPU): tables shard by bin residue
+(bin % world == rank); every rank generates its own 50M reads
+(weak scaling), hashes them, and exchanges (table, bin) records with RCCL
+all-to-all over xGMI; owners apply them.  value = all ranks' k-mers / max time.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes_per_kmer(L, k, n_tables):
+    """2-bit input per k-mer + 1 B read + 1 B write per table."""
+    return (L / 4.0) / (L - k + 1) + 2.0 * n_tables
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reads", type=int, default=50_000_000, help="reads per GPU")
+    ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("-k", type=int, default=21)
+    ap.add_argument("--tables", type=int, default=4)
+    ap.add_argument("-x", type=float, default=1e9)
+    ap.add_argument("--batch-kmers", type=int, default=1 << 28)
+    ap.add_argument("--no-bigcount", action="store_true")
+    ap.add_argument("--cpu-reads", type=int, default=1_000_000,
+                    help="reads in the oracle CPU-baseline sample (0 = skip)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def kernel_stats(lib, g):
+    buf = ctypes.create_string_buffer(1 << 16)
+    n = ctypes.c_size_t()
+    lib.kh_graph_kernel_stats(g, buf, len(buf), ctypes.byref(n))
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, cnt, ms = line.split("\t")
+        out[name] = (int(cnt), float(ms))
+    return out
+
+
+def cpu_baseline(args, sizes):
+    """The oracle (C restatement, 1 thread) on a bounded sample of the same
+    synthetic stream into the same-size tables."""
+    from oracle import oracle as O
+    from khmer_amd import synth
+    t = O.Table(O.BYTE, args.k, sizes)
+    t.set_use_bigcount(not args.no_bigcount)
+    total, secs = 0, 0.0
+    chunk = 100_000
+    for r0 in range(0, args.cpu_reads, chunk):
+        seqs, offs = synth.batch(r0, min(chunk, args.cpu_reads - r0), args.read_len)
+        offs = [int(v) for v in offs]
+        t0 = time.perf_counter()
+        total += t.consume_batch(seqs, offs)
+        secs += time.perf_counter() - t0
+    return {
+        "value": total / secs,
+        "unit": "k-mers/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": "%d synthetic %d bp reads (%d k-mers, the first reads of the benchmark stream) "
+                  "into the same 4x%.0e Countgraph, oracle/khmer_oracle.c single thread"
+                  % (args.cpu_reads, args.read_len, total, args.x),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+
+    import khmer_amd
+    from khmer_amd import _lib, synth
+    from khmer_amd._lib import lib, check
+    _lib.set_default_device(local)
+
+    L, k, nt = args.read_len, args.k, args.tables
+    nreads = args.reads
+    nkmers = nreads * (L - k + 1)
+    sizes = khmer_amd.get_n_primes_near_x(nt, args.x)
+
+    if world > 1:
+        from khmer_amd import parallel
+        runner = parallel.ShardedCountgraphBench(args, rank, world, local, sizes)
+    else:
+        runner = SingleGpuBench(args, local, sizes)
+
+    runner.setup()
+    for _ in range(args.warmup):
+        runner.step()
+    runner.sync()
+    runner.barrier()
+    runner.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        runner.step()
+    runner.sync()
+    t1 = time.perf_counter()
+    runner.barrier()
+    elapsed = runner.max_over_ranks(t1 - t0)
+    stats = runner.kernel_stats()
+    runner.profile(False)
+    check_info = runner.check()
+
+    bpk = algorithmic_bytes_per_kmer(L, k, nt)
+    total_kmers = nkmers * world * args.steps
+    value = total_kmers / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # dominant kernel and its live HIP-event average duration
+    dom = max(stats.items(), key=lambda kv: kv[1][1]) if stats else None
+    roofline = None
+    if dom:
+        name, (cnt, ms) = dom
+        avg_s = ms / 1e3 / cnt
+        kmers_per_launch = nkmers * args.steps / cnt  # per-rank k-mers one launch processes
+        achieved = bpk * kmers_per_launch / avg_s
+        traffic = None
+        try:
+            with open(args.traffic_json) as fh:
+                tj = json.load(fh)
+            if tj.get("kernel") == name and tj.get("config") == runner.config_name():
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        step_s = elapsed / args.steps
+        roofline = {
+            "bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+            "frac": achieved / PEAK_HBM, "traffic": traffic,
+            "kernel": name, "avg_launch_ms": ms / cnt, "launches": cnt,
+            "bytes_per_kmer": bpk,
+            "pipeline_frac": bpk * nkmers / step_s / PEAK_HBM,
+            "kernels_ms_per_step": {n: round(v[1] / args.steps, 3) for n, v in sorted(stats.items())},
+        }
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_reads > 0:
+        cpu = cpu_baseline(args, sizes)
+
+    if rank == 0:
+        line = {
+            "metric": "k-mers hashed/sec into Countgraph (k=21, 4x1e9)",
+            "value": value,
+            "unit": "k-mers/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded SplitMix64 reads generated in HBM)",
+            "config": {
+                "workload": runner.config_name(),
+                "k": k, "n_tables": nt, "table_sizes": sizes, "reads_per_gpu": nreads,
+                "read_len": L, "kmers_per_gpu_per_step": nkmers, "bigcount": not args.no_bigcount,
+                "batch_kmers": args.batch_kmers,
+                "parallelism": ("shard%d" % world) if world > 1 else "single",
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "check": check_info,
+        }
+        print(json.dumps(line), flush=True)
+    runner.close()
+
+
+class SingleGpuBench(object):
+    def __init__(self, args, device, sizes):
+        self.args, self.device, self.sizes = args, device, sizes
+
+    def config_name(self):
+        a = self.args
+        return "Countgraph k=%d %dx%.0e, %d x %d bp synthetic reads, 1xMI355X" % (
+            a.k, a.tables, a.x, a.reads, a.read_len)
+
+    def setup(self):
+        import khmer_amd
+        from khmer_amd import synth
+        from khmer_amd._lib import lib, check
+        a = self.args
+        self.lib, self._ck = lib, check
+        self.g = khmer_amd.Countgraph(a.k, a.x, a.tables)
+        if not a.no_bigcount:
+            self.g.set_use_bigcount(True)
+        check(lib.kh_graph_set_batch_kmers(self.g._g, a.batch_kmers))
+        self.nkmers = a.reads * (a.read_len - a.k + 1)
+        nwords = a.reads * a.read_len // 32 + 2
+        self.words, self.koff = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib.kh_device_malloc(self.device, nwords * 8, ctypes.byref(self.words)))
+        check(lib.kh_device_malloc(self.device, (a.reads + 1) * 8, ctypes.byref(self.koff)))
+        check(lib.kh_synth_packed_device(self.device, synth.SEED, 0, a.reads, a.read_len, a.k,
+                                         self.words, self.koff))
+
+    def step(self):
+        self._ck(self.lib.kh_graph_clear(self.g._g))
+        self._ck(self.lib.kh_consume_packed_device(self.g._g, self.words, self.koff,
+                                                   self.args.reads, self.nkmers))
+
+    def sync(self):
+        self._ck(self.lib.kh_device_synchronize(self.device))
+
+    def barrier(self):
+        pass
+
+    def max_over_ranks(self, t):
+        return t
+
+    def profile(self, on):
+        self._ck(self.lib.kh_graph_set_profiling(self.g._g, 1 if on else 0))
+
+    def kernel_stats(self):
+        return kernel_stats(self.lib, self.g._g)
+
+    def check(self):
+        """Counters of the last step (the full workload into empty tables)."""
+        return {"n_unique_kmers": self.g.n_unique_kmers(), "n_occupied": self.g.n_occupied()}
+
+    def close(self):
+        self.lib.kh_device_free(self.device, self.words)
+        self.lib.kh_device_free(self.device, self.koff)
+        del self.g
+
+
+if __name__ == "__main__":
+    main()

@@ -115,10 +115,11 @@ int kh_consume_parser(kh_graph *g, kh_parser *p, int mode, uint32_t *reads, uint
  * _to_valid_dna first (consume_seqfile semantics), 0 hashes raw (consume()). */
 int kh_consume_seqs(kh_graph *g, const char *seqs, const uint64_t *offsets, uint64_t nreads,
                     int clean, uint64_t *kmers);
-/* device-resident packed batch (bench / multi-GPU path): `d_words` 2-bit
+/* device-resident packed reads (bench / multi-GPU path): `d_words` 2-bit
  * packed bases (kh_device.h layout) and `d_kmer_off[nreads+1]` k-mer prefix
- * offsets, both already in this graph's device memory.  Every read must hold
- * at least one k-mer.  Asynchronous on the graph's stream. */
+ * offsets (d_kmer_off[0] == 0), both already in this graph's device memory.
+ * Every read must hold at least one k-mer.  Processed in device batches of
+ * kh_graph_set_batch_kmers() k-mers; returns when the tables are updated. */
 int kh_consume_packed_device(kh_graph *g, const uint64_t *d_words, const uint64_t *d_kmer_off,
                              uint64_t nreads, uint64_t nkmers);
 /* explicit hashes: Hashtable::count/add(HashIntoType) (include/oxli/hashtable.hh:222-243);
@@ -159,6 +160,10 @@ int kh_synth_packed_device(int device, uint64_t seed, uint64_t r0, uint64_t nrea
 int kh_device_malloc(int device, uint64_t bytes, void **out);
 int kh_device_free(int device, void *p);
 int kh_device_synchronize(int device);
+/* per-kernel HIP-event timing on the graph's stream: on=1 resets and enables;
+ * stats are text lines "kernel<TAB>launches<TAB>total_ms" */
+int kh_graph_set_profiling(kh_graph *g, int on);
+int kh_graph_kernel_stats(kh_graph *g, char *buf, size_t cap, size_t *len);
 
 #ifdef __cplusplus
 }

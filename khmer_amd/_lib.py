@@ -54,6 +54,7 @@ SIGNATURES = {
     "kh_graph_n_unique_kmers": (i32, [P, PU64]),
     "kh_graph_n_occupied": (i32, [P, PU64]),
     "kh_graph_set_batch_kmers": (i32, [P, u64]),
+    "kh_graph_clear": (i32, [P]),
     "kh_consume_parser": (i32, [P, P, i32, PU32, PU64]),
     "kh_consume_seqs": (i32, [P, ctypes.c_char_p, PU64, u64, i32, PU64]),
     "kh_consume_packed_device": (i32, [P, P, P, u64, u64]),
@@ -76,6 +77,8 @@ SIGNATURES = {
     "kh_device_malloc": (i32, [i32, u64, ctypes.POINTER(P)]),
     "kh_device_free": (i32, [i32, P]),
     "kh_device_synchronize": (i32, [i32]),
+    "kh_graph_set_profiling": (i32, [P, i32]),
+    "kh_graph_kernel_stats": (i32, [P, ctypes.c_char_p, sz, PSZ]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

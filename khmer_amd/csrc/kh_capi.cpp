@@ -762,3 +762,51 @@ extern "C" int kh_device_synchronize(int device) {
         KH_HIP(hipDeviceSynchronize());
     });
 }
+
+extern "C" int kh_graph_set_profiling(kh_graph *h, int on) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        g->profile = on != 0;
+        g->kstats.clear();
+    });
+}
+
+extern "C" int kh_graph_kernel_stats(kh_graph *h, char *buf, size_t cap, size_t *len) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        std::string s;
+        char line[256];
+        for (auto &kv : g->kstats) {
+            snprintf(line, sizeof line, "%s\t%llu\t%.6f\n", kv.first.c_str(), (unsigned long long)kv.second.n,
+                     kv.second.ms);
+            s += line;
+        }
+        *len = s.size();
+        if (buf && cap) {
+            size_t n = std::min(cap - 1, s.size());
+            memcpy(buf, s.data(), n);
+            buf[n] = 0;
+        }
+    });
+}
+
+// reset a graph to its freshly constructed state (tables zeroed, counters,
+// bigcounts and tags cleared) -- the benchmark's per-step reset
+extern "C" int kh_graph_clear(kh_graph *h) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        KH_HIP(hipMemsetAsync(g->d_tab, 0, g->arena_bytes, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+        g->n_unique = g->n_occupied = 0;
+        g->bigcounts.clear();
+        g->bc_dirty = true;
+        g->tags.clear();
+    });
+}

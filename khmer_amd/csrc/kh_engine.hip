@@ -46,14 +46,19 @@ constexpr uint32_t NO_J = 0xFFFFFFFFu;
 
 // ---------------------------------------------------------------------------
 // k-mer sources
+// A batch is a sub-range of a read set: `koff` points at the sub-range's
+// k-mer offsets (absolute values), kbase = koff[0], rbase = index of its first
+// read in the packed stream (base of read r = koff[r] + r*(k-1)).  Batch-local
+// k-mer j is absolute k-mer kbase + j.
 struct SrcTwoBit {
     const uint64_t *words;
     const uint64_t *koff;
     uint64_t nreads;
     int k;
+    uint64_t kbase, rbase;
     static constexpr bool kReads = true;
     __device__ __forceinline__ uint64_t hash(uint64_t j, uint64_t r) const {
-        uint64_t pos = j + r * (uint64_t)(k - 1);
+        uint64_t pos = (j + kbase) + (r + rbase) * (uint64_t)(k - 1);
         return canonical2(window2(words, pos, k), k);
     }
 };
@@ -62,9 +67,10 @@ struct SrcBytes {
     const uint64_t *koff;
     uint64_t nreads;
     int k;
+    uint64_t kbase, rbase;
     static constexpr bool kReads = true;
     __device__ __forceinline__ uint64_t hash(uint64_t j, uint64_t r) const {
-        uint64_t pos = j + r * (uint64_t)(k - 1);
+        uint64_t pos = (j + kbase) + (r + rbase) * (uint64_t)(k - 1);
         return murmur_canonical(bytes + pos, k);
     }
 };
@@ -73,6 +79,7 @@ struct SrcHashes {
     const uint64_t *koff;
     uint64_t nreads;
     int k;
+    uint64_t kbase, rbase;
     static constexpr bool kReads = false;
     __device__ __forceinline__ uint64_t hash(uint64_t j, uint64_t) const { return h[j]; }
 };
@@ -89,10 +96,11 @@ __device__ __forceinline__ TileReads load_tile_reads(const Src &src, uint64_t j0
     TileReads tr{0, 0};
     if constexpr (Src::kReads) {
         if (threadIdx.x == 0) {
-            uint64_t lo = 0, hi = src.nreads;  // koff[lo] <= j0 < koff[hi]
+            const uint64_t ja = j0 + src.kbase;
+            uint64_t lo = 0, hi = src.nreads;  // koff[lo] <= ja < koff[hi]
             while (hi - lo > 1) {
                 uint64_t mid = (lo + hi) >> 1;
-                if (src.koff[mid] <= j0) lo = mid; else hi = mid;
+                if (src.koff[mid] <= ja) lo = mid; else hi = mid;
             }
             uint64_t cnt = src.nreads - lo;
             if (cnt > j1 - j0) cnt = j1 - j0;
@@ -121,7 +129,7 @@ template <class Src>
 __device__ __forceinline__ uint64_t kmer_hash(const Src &src, const uint64_t *s_koff, const TileReads &tr,
                                               uint64_t j) {
     uint64_t r = 0;
-    if constexpr (Src::kReads) r = find_read(s_koff, tr, j);
+    if constexpr (Src::kReads) r = find_read(s_koff, tr, j + src.kbase);
     return src.hash(j, r);
 }
 
@@ -699,6 +707,31 @@ __global__ void __launch_bounds__(FIN_THREADS) k_kmer_counts(Params P, Src src, 
         out[j] = (uint16_t)get_count_dev(P, tab, kmer_hash(src, s_koff, tr, j), bc_keys, bc_vals, bc_n);
 }
 
+// Correctly rounded float32 division and square root.  The device's native
+// f32 sqrt is not correctly rounded (1 ulp), so both start from a double
+// estimate and are fixed up against the exact float midpoints: a midpoint has
+// 25 significant bits, so midpoint*b (b a float) and midpoint^2 are exact in
+// double, and ties cannot occur for these operations.
+__device__ __forceinline__ float div_rn_exact(float a, float b) {   // b > 0
+    float q = (float)((double)a / (double)b);
+    const float dn = nextafterf(q, -INFINITY), up = nextafterf(q, INFINITY);
+    const double lo = ((double)q + (double)dn) * 0.5, hi = ((double)q + (double)up) * 0.5;
+    const double ad = (double)a, bd = (double)b;
+    if (ad < lo * bd) q = dn;
+    else if (ad > hi * bd) q = up;
+    return q;
+}
+__device__ __forceinline__ float sqrt_rn_exact(float x) {           // x >= 0
+    if (x == 0.f) return x;
+    float r = (float)sqrt((double)x);
+    const float dn = nextafterf(r, 0.f), up = nextafterf(r, INFINITY);
+    const double lo = ((double)r + (double)dn) * 0.5, hi = ((double)r + (double)up) * 0.5;
+    const double xd = (double)x;
+    if (xd < lo * lo) r = dn;
+    else if (xd > hi * hi) r = up;
+    return r;
+}
+
 // Hashtable::get_median_count (src/oxli/hashtable.cc:299-328): one thread per
 // read; float32 in the reference's sequential order with round-to-nearest
 // intrinsics (no contraction), IEEE sqrt, median = sorted[n/2].
@@ -710,14 +743,14 @@ __global__ void k_median(const uint64_t *koff, uint64_t nreads, uint16_t *counts
         uint16_t *c = counts + a;
         float average = 0.f;
         for (uint64_t t = 0; t < n; t++) average = __fadd_rn(average, (float)c[t]);
-        average = __fdiv_rn(average, (float)n);
+        average = div_rn_exact(average, (float)n);
         float s = 0.f;
         for (uint64_t t = 0; t < n; t++) {
             const float d = __fsub_rn((float)c[t], average);
             s = __fadd_rn(s, __fmul_rn(d, d));
         }
-        s = __fdiv_rn(s, (float)n);
-        s = __fsqrt_rn(s);
+        s = div_rn_exact(s, (float)n);
+        s = sqrt_rn_exact(s);
         // in-place heapsort of the read's counts, then the middle element
         uint64_t m = n;
         auto sift = [&](uint64_t root, uint64_t end) {
@@ -839,6 +872,46 @@ void engine_sync_bigcounts(Graph *g) {
     g->bc_dirty = false;
 }
 
+// ---- per-kernel HIP-event timing (bench / roofline) ----
+static hipEvent_t ev_get(Graph *g) {
+    if (g->ev_next == g->ev_pool.size()) {
+        hipEvent_t e;
+        KH_HIP(hipEventCreate(&e));
+        g->ev_pool.push_back(e);
+    }
+    return g->ev_pool[g->ev_next++];
+}
+struct KTimer {
+    Graph *g;
+    const char *name;
+    hipEvent_t a = nullptr;
+    KTimer(Graph *g_, const char *n) : g(g_), name(n) {
+        if (g->profile) { a = ev_get(g); KH_HIP(hipEventRecord(a, g->stream)); }
+    }
+    ~KTimer() noexcept(false) {
+        if (a) {
+            hipEvent_t b = ev_get(g);
+            KH_HIP(hipEventRecord(b, g->stream));
+            g->ev_pending.push_back({name, {a, b}});
+        }
+    }
+};
+void engine_collect_events(Graph *g) {
+    if (g->ev_pending.empty()) { g->ev_next = 0; return; }
+    KH_HIP(hipStreamSynchronize(g->stream));
+    for (auto &p : g->ev_pending) {
+        float ms = 0;
+        KH_HIP(hipEventElapsedTime(&ms, p.second.first, p.second.second));
+        auto it = std::find_if(g->kstats.begin(), g->kstats.end(), [&](auto &x) { return x.first == p.first; });
+        if (it == g->kstats.end()) { g->kstats.push_back({p.first, Graph::KStat{}}); it = g->kstats.end() - 1; }
+        it->second.ms += ms;
+        it->second.n += 1;
+    }
+    g->ev_pending.clear();
+    g->ev_next = 0;
+}
+#define TIMED(name, ...) do { KTimer kt_(g, name); __VA_ARGS__; } while (0)
+
 template <class Src>
 static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *out) {
     if (nkmers == 0) return;
@@ -859,20 +932,21 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
     int tile_kmers = L1_TILE_RECS / P.n;
     if (tile_kmers < 1) tile_kmers = 1;
     const uint64_t ntiles1 = (nkmers + tile_kmers - 1) / tile_kmers;
-    hipLaunchKernelGGL(k_count_l1<Src>, dim3((unsigned)ntiles1), dim3(L1_THREADS), lds_count_l1(P, tile_kmers), st, P,
-                       src, nkmers, tile_kmers, w.cnt1);
-    hipLaunchKernelGGL(k_scan_l1, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1, w.cnt1, w.off1, w.cur1,
-                       w.tile1);
-    hipLaunchKernelGGL(k_scatter_l1<Src>, dim3((unsigned)ntiles1), dim3(L1_THREADS), lds_scatter_l1(P, tile_kmers),
-                       st, P, src, nkmers, tile_kmers, w.cur1, w.rec1_off, w.rec1_j);
+    TIMED("count_l1", hipLaunchKernelGGL(k_count_l1<Src>, dim3((unsigned)ntiles1), dim3(L1_THREADS),
+                                         lds_count_l1(P, tile_kmers), st, P, src, nkmers, tile_kmers, w.cnt1));
+    TIMED("scan_l1", hipLaunchKernelGGL(k_scan_l1, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1,
+                                        w.cnt1, w.off1, w.cur1, w.tile1));
+    TIMED("scatter_l1", hipLaunchKernelGGL(k_scatter_l1<Src>, dim3((unsigned)ntiles1), dim3(L1_THREADS),
+                                           lds_scatter_l1(P, tile_kmers), st, P, src, nkmers, tile_kmers, w.cur1,
+                                           w.rec1_off, w.rec1_j));
     const uint64_t ntiles2 = (recs + L2_TILE_RECS - 1) / L2_TILE_RECS + F1;
-    hipLaunchKernelGGL(k_count_l2, dim3((unsigned)ntiles2), dim3(L2_THREADS), F2 * 4, st, (uint32_t)F1, P.s0, P.s2,
-                       w.off1, w.tile1, w.rec1_off, w.cnt2);
-    hipLaunchKernelGGL(k_scan_l2, dim3((unsigned)F1), dim3(1024), F2 * 8 + 1025 * 8, st, P.s2, (uint32_t)F1, w.off1,
-                       w.cnt2, w.off2, w.cur2);
-    hipLaunchKernelGGL(k_scatter_l2, dim3((unsigned)ntiles2), dim3(L2_THREADS),
-                       F2 * 8 + F2 * 4 * 3 + L2_TILE_RECS * 10, st, (uint32_t)F1, P.s0, P.s2, w.off1, w.tile1, w.cur2,
-                       w.rec1_off, w.rec1_j, w.rec2_off, w.rec2_j);
+    TIMED("count_l2", hipLaunchKernelGGL(k_count_l2, dim3((unsigned)ntiles2), dim3(L2_THREADS), F2 * 4, st,
+                                         (uint32_t)F1, P.s0, P.s2, w.off1, w.tile1, w.rec1_off, w.cnt2));
+    TIMED("scan_l2", hipLaunchKernelGGL(k_scan_l2, dim3((unsigned)F1), dim3(1024), F2 * 8 + 1025 * 8, st, P.s2,
+                                        (uint32_t)F1, w.off1, w.cnt2, w.off2, w.cur2));
+    TIMED("scatter_l2", hipLaunchKernelGGL(k_scatter_l2, dim3((unsigned)ntiles2), dim3(L2_THREADS),
+                                           F2 * 8 + F2 * 4 * 3 + L2_TILE_RECS * 10, st, (uint32_t)F1, P.s0, P.s2,
+                                           w.off1, w.tile1, w.cur2, w.rec1_off, w.rec1_j, w.rec2_off, w.rec2_j));
 
     ApplyArgs A;
     A.off2 = w.off2;
@@ -890,14 +964,16 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
     const uint64_t real_regions = A.rprefix[P.n];
     const unsigned agrid = (unsigned)std::min<uint64_t>(real_regions, 256 * 8);
     if (P.kind == BIT)
-        hipLaunchKernelGGL(k_apply_bit, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P), st, P, A);
+        TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P), st, P, A));
     else if (P.kind == NIBBLE)
-        hipLaunchKernelGGL(k_apply_count<NIBBLE>, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P), st, P, A);
+        TIMED("apply_nibble", hipLaunchKernelGGL(k_apply_count<NIBBLE>, dim3(agrid), dim3(APPLY_THREADS),
+                                                 lds_apply(P), st, P, A));
     else
-        hipLaunchKernelGGL(k_apply_count<BYTE>, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P), st, P, A);
+        TIMED("apply_byte", hipLaunchKernelGGL(k_apply_count<BYTE>, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P),
+                                               st, P, A));
     if (P.kind == BYTE && P.use_bigcount)
-        hipLaunchKernelGGL(k_crossing, dim3(1024), dim3(256), 0, st, P, w.off2, w.rec2_off, w.rec2_j, w.cross, w.ctr,
-                           w.cap_cross, w.fullf);
+        TIMED("crossing", hipLaunchKernelGGL(k_crossing, dim3(1024), dim3(256), 0, st, P, w.off2, w.rec2_off,
+                                             w.rec2_j, w.cross, w.ctr, w.cap_cross, w.fullf));
 
     uint8_t *d_out_new = nullptr;
     uint64_t *d_out_hash = nullptr;
@@ -908,13 +984,15 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
         else KH_HIP(hipMalloc((void **)&d_out_hash, nkmers * 8));
     }
     const uint64_t fin_tiles = (nkmers + FIN_TILE - 1) / FIN_TILE;
-    hipLaunchKernelGGL(k_finalize<Src>, dim3((unsigned)fin_tiles), dim3(FIN_THREADS), 16 + (FIN_TILE + 2) * 8, st, P,
-                       src, nkmers, w.newf, w.fullf, w.ctr, w.bc, w.cap_bc, (uint8_t *)nullptr, d_out_hash);
+    TIMED("finalize", hipLaunchKernelGGL(k_finalize<Src>, dim3((unsigned)fin_tiles), dim3(FIN_THREADS),
+                                         16 + (FIN_TILE + 2) * 8, st, P, src, nkmers, w.newf, w.fullf, w.ctr, w.bc,
+                                         w.cap_bc, (uint8_t *)nullptr, d_out_hash));
     KH_HIP(hipGetLastError());
     KH_HIP(hipMemcpyAsync(w.h_ctr, w.ctr, CTR_N * 8, hipMemcpyDeviceToHost, st));
     if (d_out_new) KH_HIP(hipMemcpyAsync(out->h_new, d_out_new, nkmers, hipMemcpyDeviceToHost, st));
     if (d_out_hash) KH_HIP(hipMemcpyAsync(out->h_hash, d_out_hash, nkmers * 8, hipMemcpyDeviceToHost, st));
     KH_HIP(hipStreamSynchronize(st));
+    engine_collect_events(g);
     if (d_out_hash && d_out_hash != (uint64_t *)w.rec1_off) KH_HIP(hipFree(d_out_hash));
     if (w.h_ctr[CTR_ERR]) fail(KH_EDEVICE, "device overflow of crossing/bigcount buffers");
     g->n_occupied += w.h_ctr[CTR_OCC];
@@ -939,21 +1017,86 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
     }
 }
 
+// batch boundaries of a device read set: chunk i starts at the last read whose
+// k-mer offset is <= koff[0] + i*B
+__global__ void k_chunk_bounds(const uint64_t *koff, uint64_t nreads, uint64_t B, uint64_t nchunks,
+                               uint64_t *out_r, uint64_t *out_k) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i <= nchunks;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t r;
+        if (i == nchunks) {
+            r = nreads;
+        } else {
+            const uint64_t target = koff[0] + i * B;
+            uint64_t lo = 0, hi = nreads;  // koff[lo] <= target
+            while (hi - lo > 1) {
+                uint64_t mid = (lo + hi) >> 1;
+                if (koff[mid] <= target) lo = mid; else hi = mid;
+            }
+            r = lo;
+        }
+        out_r[i] = r;
+        out_k[i] = koff[r];
+    }
+}
+
+template <class Src>
+static void consume_reads_chunked(Graph *g, Src base, const uint64_t *d_koff, uint64_t nreads, uint64_t nkmers,
+                                  const PassOut *out) {
+    if (nkmers == 0 || nreads == 0) return;
+    const uint64_t B = g->batch_kmers;
+    if (out || nkmers <= B + (B >> 4)) {   // one pass (koff[0] == 0 by contract)
+        Src s = base;
+        s.koff = d_koff;
+        s.nreads = nreads;
+        run_pass(g, s, nkmers, out);
+        return;
+    }
+    const uint64_t nchunks = (nkmers + B - 1) / B;
+    std::vector<uint64_t> rr(nchunks + 1), kk(nchunks + 1);
+    uint64_t *d = nullptr;
+    KH_HIP(hipMalloc((void **)&d, (nchunks + 1) * 16));
+    hipLaunchKernelGGL(k_chunk_bounds, dim3((unsigned)std::min<uint64_t>((nchunks + 256) / 256, 4096)), dim3(256), 0,
+                       g->stream, d_koff, nreads, B, nchunks, d, d + nchunks + 1);
+    KH_HIP(hipGetLastError());
+    KH_HIP(hipMemcpyAsync(rr.data(), d, (nchunks + 1) * 8, hipMemcpyDeviceToHost, g->stream));
+    KH_HIP(hipMemcpyAsync(kk.data(), d + nchunks + 1, (nchunks + 1) * 8, hipMemcpyDeviceToHost, g->stream));
+    KH_HIP(hipStreamSynchronize(g->stream));
+    KH_HIP(hipFree(d));
+    uint64_t done = 0;
+    for (uint64_t i = 0; i < nchunks; i++) {
+        uint64_t r0 = rr[i], r1 = rr[i + 1];
+        if (r1 <= r0) continue;  // a read longer than a batch: merged into the next chunk
+        Src s = base;
+        s.koff = d_koff + r0;
+        s.nreads = r1 - r0;
+        s.kbase = kk[i];
+        s.rbase = r0;
+        run_pass(g, s, kk[i + 1] - kk[i], out);
+        done += kk[i + 1] - kk[i];
+    }
+    if (done != nkmers) fail(KH_EVALUE, "k-mer offsets do not match the k-mer count");
+}
+
 void engine_consume_twobit(Graph *g, const uint64_t *d_words, const uint64_t *d_koff, uint64_t nreads,
                            uint64_t nkmers, const PassOut *out) {
-    SrcTwoBit s{d_words, d_koff, nreads, g->k};
-    run_pass(g, s, nkmers, out);
+    SrcTwoBit s{d_words, d_koff, nreads, g->k, 0, 0};
+    consume_reads_chunked(g, s, d_koff, nreads, nkmers, out);
 }
 
 void engine_consume_bytes(Graph *g, const uint8_t *d_bytes, const uint64_t *d_koff, uint64_t nreads,
                           uint64_t nkmers, const PassOut *out) {
-    SrcBytes s{d_bytes, d_koff, nreads, g->k};
-    run_pass(g, s, nkmers, out);
+    SrcBytes s{d_bytes, d_koff, nreads, g->k, 0, 0};
+    consume_reads_chunked(g, s, d_koff, nreads, nkmers, out);
 }
 
 void engine_consume_hashes(Graph *g, const uint64_t *d_hashes, uint64_t n, const PassOut *out) {
-    SrcHashes s{d_hashes, nullptr, 0, g->k};
-    run_pass(g, s, n, out);
+    const uint64_t B = g->batch_kmers;
+    if (n > B && out) fail(KH_EVALUE, "per-k-mer outputs need a single device batch");
+    for (uint64_t a = 0; a < n; a += B) {
+        SrcHashes s{d_hashes + a, nullptr, 0, g->k, 0, 0};
+        run_pass(g, s, std::min(B, n - a), out);
+    }
 }
 
 static void upload_batch(Graph *g, const HostBatch &b) {
@@ -986,11 +1129,11 @@ void engine_hash_batch(Graph *g, const HostBatch &b, uint64_t *h_out) {
     KH_HIP(hipMalloc((void **)&d, nk * 8));
     const uint64_t tiles = (nk + FIN_TILE - 1) / FIN_TILE;
     if (b.hash == MURMUR) {
-        SrcBytes s{g->ws.d_bytes, g->ws.d_koff, nr, g->k};
+        SrcBytes s{g->ws.d_bytes, g->ws.d_koff, nr, g->k, 0, 0};
         hipLaunchKernelGGL(k_kmer_hashes<SrcBytes>, dim3((unsigned)tiles), dim3(FIN_THREADS), 16 + (FIN_TILE + 2) * 8,
                            g->stream, s, nk, d);
     } else {
-        SrcTwoBit s{g->ws.d_words, g->ws.d_koff, nr, g->k};
+        SrcTwoBit s{g->ws.d_words, g->ws.d_koff, nr, g->k, 0, 0};
         hipLaunchKernelGGL(k_kmer_hashes<SrcTwoBit>, dim3((unsigned)tiles), dim3(FIN_THREADS), 16 + (FIN_TILE + 2) * 8,
                            g->stream, s, nk, d);
     }
@@ -1032,12 +1175,12 @@ void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, floa
     const uint64_t tiles = (nk + FIN_TILE - 1) / FIN_TILE;
     if (tiles) {
         if (b.hash == MURMUR) {
-            SrcBytes s{g->ws.d_bytes, g->ws.d_koff, nr, g->k};
+            SrcBytes s{g->ws.d_bytes, g->ws.d_koff, nr, g->k, 0, 0};
             hipLaunchKernelGGL(k_kmer_counts<SrcBytes>, dim3((unsigned)tiles), dim3(FIN_THREADS),
                                16 + (FIN_TILE + 2) * 8, g->stream, g->prm, s, nk, g->d_tab, d_counts, g->d_bc_keys,
                                g->d_bc_vals, g->d_bc_n);
         } else {
-            SrcTwoBit s{g->ws.d_words, g->ws.d_koff, nr, g->k};
+            SrcTwoBit s{g->ws.d_words, g->ws.d_koff, nr, g->k, 0, 0};
             hipLaunchKernelGGL(k_kmer_counts<SrcTwoBit>, dim3((unsigned)tiles), dim3(FIN_THREADS),
                                16 + (FIN_TILE + 2) * 8, g->stream, g->prm, s, nk, g->d_tab, d_counts, g->d_bc_keys,
                                g->d_bc_vals, g->d_bc_n);
@@ -1205,6 +1348,7 @@ Graph::~Graph() {
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (w.h_ctr) (void)hipHostFree(w.h_ctr);
+    for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
 }
 

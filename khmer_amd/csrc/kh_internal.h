@@ -107,6 +107,13 @@ struct Graph {
     std::unordered_set<uint64_t> tags;                  // hashgraph.hh:113 all_tags
     uint64_t batch_kmers = 1ull << 27;
     Workspace ws;
+    // optional per-kernel HIP-event timing (kh_graph_set_profiling)
+    bool profile = false;
+    struct KStat { double ms = 0; uint64_t n = 0; };
+    std::vector<std::pair<std::string, KStat>> kstats;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
+    size_t ev_next = 0;
     std::recursive_mutex mu;
     ~Graph();
 };
@@ -168,5 +175,6 @@ void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, floa
 void engine_sync_bigcounts(Graph *g);
 void engine_download_table(Graph *g, int i, uint8_t *dst);
 void engine_upload_table(Graph *g, int i, const uint8_t *src);
+void engine_collect_events(Graph *g);
 
 }  // namespace kh

@@ -255,8 +255,12 @@ or_table *or_table_new(int kind, int hash, int k, const uint64_t *sizes, int n) 
         t->sizes[i] = sizes[i];
         /* allocation sizes: storage.hh:127-140 (bit), :297-310 (nibble), :502-511 (byte) */
         t->nbytes[i] = kind == OR_BIT ? sizes[i] / 8 + 1 : kind == OR_NIBBLE ? sizes[i] / 2 + 1 : sizes[i];
-        t->tab[i] = calloc(t->nbytes[i] ? t->nbytes[i] : 1, 1);
+        /* allocate + memset like the reference (storage.hh:502-511): pages are
+         * touched at construction, not inside a timed consume */
+        t->tab[i] = malloc(t->nbytes[i] ? t->nbytes[i] : 1);
         if (!t->tab[i]) { set_err("out of memory"); or_table_free(t); return NULL; }
+        memset(t->tab[i], 0, t->nbytes[i] ? t->nbytes[i] : 1);
+        for (uint64_t b = 0; b < t->nbytes[i]; b += 4096) ((volatile uint8_t *)t->tab[i])[b] = 0;
     }
     return t;
 }
