@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("-x", type=float, default=1e9)
     ap.add_argument("--batch-kmers", type=int, default=1 << 28)
     ap.add_argument("--no-bigcount", action="store_true")
+    ap.add_argument("--variable-path", action="store_true",
+                    help="feed k-mer offsets (variable-length read path) instead of the fixed-length path")
     ap.add_argument("--cpu-reads", type=int, default=1_000_000,
                     help="reads in the oracle CPU-baseline sample (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -223,8 +225,12 @@ class SingleGpuBench(object):
 
     def step(self):
         self._ck(self.lib.kh_graph_clear(self.g._g))
-        self._ck(self.lib.kh_consume_packed_device(self.g._g, self.words, self.koff,
-                                                   self.args.reads, self.nkmers))
+        if self.args.variable_path:
+            self._ck(self.lib.kh_consume_packed_device(self.g._g, self.words, self.koff,
+                                                       self.args.reads, self.nkmers))
+        else:
+            self._ck(self.lib.kh_consume_packed_fixed_device(self.g._g, self.words, self.args.reads,
+                                                             self.args.read_len))
 
     def sync(self):
         self._ck(self.lib.kh_device_synchronize(self.device))

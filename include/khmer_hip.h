@@ -103,6 +103,8 @@ int  kh_graph_n_unique_kmers(kh_graph *g, uint64_t *out);      /* storage.hh:143
 int  kh_graph_n_occupied(kh_graph *g, uint64_t *out);
 /* largest k-mer batch processed per device pipeline pass (memory knob) */
 int  kh_graph_set_batch_kmers(kh_graph *g, uint64_t max_kmers);
+/* back to the freshly constructed state (zero tables, counters, bigcounts, tags) */
+int  kh_graph_clear(kh_graph *g);
 
 /* ---------------- hot path: consume ----------------------------------------
  * Hashtable::consume_seqfile<FastxReader> (src/oxli/hashtable.cc:125-150):
@@ -122,6 +124,9 @@ int kh_consume_seqs(kh_graph *g, const char *seqs, const uint64_t *offsets, uint
  * kh_graph_set_batch_kmers() k-mers; returns when the tables are updated. */
 int kh_consume_packed_device(kh_graph *g, const uint64_t *d_words, const uint64_t *d_kmer_off,
                              uint64_t nreads, uint64_t nkmers);
+/* the same for reads of one length (read_len >= k): no offset array, read r
+ * starts at base r*read_len (the common fixed-length sequencing case). */
+int kh_consume_packed_fixed_device(kh_graph *g, const uint64_t *d_words, uint64_t nreads, uint32_t read_len);
 /* explicit hashes: Hashtable::count/add(HashIntoType) (include/oxli/hashtable.hh:222-243);
  * is_new[n] (nullable) receives Storage::add's return per hash, in order. */
 int kh_add_hashes(kh_graph *g, const uint64_t *hashes, uint64_t n, uint8_t *is_new);

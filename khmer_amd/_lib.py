@@ -58,6 +58,7 @@ SIGNATURES = {
     "kh_consume_parser": (i32, [P, P, i32, PU32, PU64]),
     "kh_consume_seqs": (i32, [P, ctypes.c_char_p, PU64, u64, i32, PU64]),
     "kh_consume_packed_device": (i32, [P, P, P, u64, u64]),
+    "kh_consume_packed_fixed_device": (i32, [P, P, u64, u32]),
     "kh_add_hashes": (i32, [P, PU64, u64, ctypes.POINTER(ctypes.c_uint8)]),
     "kh_get_counts": (i32, [P, PU64, u64, ctypes.POINTER(ctypes.c_uint16)]),
     "kh_median_counts": (i32, [P, ctypes.c_char_p, PU64, u64, ctypes.POINTER(ctypes.c_uint16),

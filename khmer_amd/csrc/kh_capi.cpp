@@ -348,6 +348,17 @@ int kh_consume_packed_device(kh_graph *h, const uint64_t *d_words, const uint64_
     });
 }
 
+int kh_consume_packed_fixed_device(kh_graph *h, const uint64_t *d_words, uint64_t nreads, uint32_t read_len) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        if (g->hash != TWOBIT) fail(KH_EVALUE, "packed 2-bit input requires a 2-bit hashing graph");
+        engine_consume_twobit_fixed(g, d_words, nreads, read_len, nullptr);
+    });
+}
+
 int kh_add_hashes(kh_graph *h, const uint64_t *hashes, uint64_t n, uint8_t *is_new) {
     return guard([&] {
         CHECK_PTR(h);

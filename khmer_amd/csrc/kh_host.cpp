@@ -138,6 +138,7 @@ void HostBatch::append(const char *s, size_t len, int k, bool clean) {
             i++; p++;
         }
     }
+    if (!read_kmers.empty() && read_kmers.back() != nk) uniform = false;
     nbases += len;
     koff.push_back(koff.back() + nk);
     read_kmers.push_back((uint32_t)nk);

@@ -64,8 +64,7 @@ struct Params {
 // device workspace of one pipeline pass (grown on demand)
 struct Workspace {
     uint64_t cap_kmers = 0, cap_recs = 0;
-    uint32_t *rec1_off = nullptr, *rec1_j = nullptr;
-    uint32_t *rec2_off = nullptr, *rec2_j = nullptr;
+    uint64_t *rec1 = nullptr, *rec2 = nullptr;   // (k-mer index << 32) | bin offset
     uint8_t *newf = nullptr, *fullf = nullptr;   // per k-mer flags
     uint64_t *bc = nullptr;                      // bigcount candidate hashes
     uint64_t *hashes_out = nullptr;              // optional per-k-mer hashes
@@ -85,6 +84,10 @@ struct Workspace {
     uint64_t *d_words = nullptr, *d_koff = nullptr;
     uint8_t *d_bytes = nullptr;
     uint64_t cap_words = 0, cap_koff = 0, cap_bytes = 0;
+    // query staging
+    uint64_t *q_hashes = nullptr;
+    uint16_t *q_counts = nullptr;
+    uint64_t cap_q = 0, cap_q16 = 0;
 };
 enum { CTR_OCC = 0, CTR_UNIQUE, CTR_NCROSS, CTR_NBC, CTR_ERR, CTR_N };
 
@@ -136,10 +139,11 @@ struct HostBatch {
     std::vector<uint64_t> koff{0};   // k-mer prefix offsets per packed read
     std::vector<uint32_t> read_kmers;  // per packed read
     uint64_t nbases = 0;
+    bool uniform = true;             // every packed read has the same length
     uint64_t nkmers() const { return koff.back(); }
     uint64_t nreads() const { return koff.size() - 1; }
     void clear() {
-        words.clear(); bytes.clear(); koff.assign(1, 0); read_kmers.clear(); nbases = 0;
+        words.clear(); bytes.clear(); koff.assign(1, 0); read_kmers.clear(); nbases = 0; uniform = true;
     }
     // append a read (reads shorter than k are skipped by the caller)
     void append(const char *s, size_t len, int k, bool clean);
@@ -166,6 +170,8 @@ struct PassOut {
 };
 void engine_consume_twobit(Graph *g, const uint64_t *d_words, const uint64_t *d_koff,
                            uint64_t nreads, uint64_t nkmers, const PassOut *out);
+void engine_consume_twobit_fixed(Graph *g, const uint64_t *d_words, uint64_t nreads, uint64_t read_len,
+                                 const PassOut *out);
 void engine_consume_bytes(Graph *g, const uint8_t *d_bytes, const uint64_t *d_koff,
                           uint64_t nreads, uint64_t nkmers, const PassOut *out);
 void engine_consume_hashes(Graph *g, const uint64_t *d_hashes, uint64_t n, const PassOut *out);

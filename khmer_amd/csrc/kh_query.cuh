@@ -1,0 +1,212 @@
+// kh_query.cuh -- read-only device kernels: get_count, k-mer hashes/counts,
+// get_median_count, batch boundaries, synthetic reads.  Included by kh_engine.hip.
+#pragma once
+#include "kh_src.cuh"
+
+namespace kh {
+
+constexpr int Q_THREADS = 256;
+constexpr int Q_TILE = 2048;
+
+// ---------------------------------------------------------------------------
+// queries: Storage::get_count (storage.hh:206-219, 362-379, 627-649)
+__device__ __forceinline__ uint32_t get_count_dev(const Params &P, const uint8_t *tab, uint64_t h,
+                                                  const uint64_t *bc_keys, const uint16_t *bc_vals,
+                                                  uint64_t bc_n) {
+    if (P.kind == BIT) {
+        for (int i = 0; i < P.n; i++) {
+            const uint64_t bin = mod_barrett(h, P.p[i], P.m[i]);
+            if (!((tab[P.tbyte[i] + (bin >> 3)] >> (bin & 7)) & 1)) return 0;
+        }
+        return 1;
+    }
+    if (P.kind == NIBBLE) {
+        uint32_t mn = 15;
+        for (int i = 0; i < P.n; i++) {
+            const uint64_t bin = mod_barrett(h, P.p[i], P.m[i]);
+            const uint8_t byte = tab[P.tbyte[i] + (bin >> 1)];
+            const uint32_t c = (bin & 1) ? (byte & 0x0F) : (byte >> 4);
+            mn = c < mn ? c : mn;
+        }
+        return mn;
+    }
+    uint32_t mn = 255;
+    for (int i = 0; i < P.n; i++) {
+        const uint32_t c = tab[P.tbyte[i] + mod_barrett(h, P.p[i], P.m[i])];
+        mn = c < mn ? c : mn;
+    }
+    if (mn == 255 && P.use_bigcount && bc_n) {
+        uint64_t lo = 0, hi = bc_n;
+        while (lo < hi) {
+            uint64_t mid = (lo + hi) >> 1;
+            if (bc_keys[mid] < h) lo = mid + 1; else hi = mid;
+        }
+        if (lo < bc_n && bc_keys[lo] == h) mn = bc_vals[lo];
+    }
+    return mn;
+}
+
+__global__ void k_get_counts(Params P, const uint8_t *tab, const uint64_t *hashes, uint64_t n, uint16_t *out,
+                             const uint64_t *bc_keys, const uint16_t *bc_vals, uint64_t bc_n) {
+    for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < n; q += (uint64_t)gridDim.x * blockDim.x)
+        out[q] = (uint16_t)get_count_dev(P, tab, hashes[q], bc_keys, bc_vals, bc_n);
+}
+
+// hashes of every k-mer of a batch
+template <class Src>
+__global__ void __launch_bounds__(Q_THREADS) k_kmer_hashes(Src src, uint64_t nkmers, uint64_t *out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *s_meta = (uint64_t *)smem;
+    uint64_t *s_koff = s_meta + 2;
+    const uint64_t j0 = (uint64_t)blockIdx.x * Q_TILE;
+    const uint64_t j1 = min(nkmers, j0 + Q_TILE);
+    TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
+    __syncthreads();
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) out[j] = kmer_hash(src, s_koff, tr, j);
+}
+
+// counts of every k-mer of a batch (for get_median_count)
+template <class Src>
+__global__ void __launch_bounds__(Q_THREADS) k_kmer_counts(Params P, Src src, uint64_t nkmers, const uint8_t *tab,
+                                                            uint16_t *out, const uint64_t *bc_keys,
+                                                            const uint16_t *bc_vals, uint64_t bc_n) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *s_meta = (uint64_t *)smem;
+    uint64_t *s_koff = s_meta + 2;
+    const uint64_t j0 = (uint64_t)blockIdx.x * Q_TILE;
+    const uint64_t j1 = min(nkmers, j0 + Q_TILE);
+    TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
+    __syncthreads();
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x)
+        out[j] = (uint16_t)get_count_dev(P, tab, kmer_hash(src, s_koff, tr, j), bc_keys, bc_vals, bc_n);
+}
+
+// Correctly rounded float32 division and square root.  The device's native
+// f32 sqrt is not correctly rounded (1 ulp), so both start from a double
+// estimate and are fixed up against the exact float midpoints: a midpoint has
+// 25 significant bits, so midpoint*b (b a float) and midpoint^2 are exact in
+// double, and ties cannot occur for these operations.
+__device__ __forceinline__ float div_rn_exact(float a, float b) {   // b > 0
+    float q = (float)((double)a / (double)b);
+    const float dn = nextafterf(q, -INFINITY), up = nextafterf(q, INFINITY);
+    const double lo = ((double)q + (double)dn) * 0.5, hi = ((double)q + (double)up) * 0.5;
+    const double ad = (double)a, bd = (double)b;
+    if (ad < lo * bd) q = dn;
+    else if (ad > hi * bd) q = up;
+    return q;
+}
+__device__ __forceinline__ float sqrt_rn_exact(float x) {           // x >= 0
+    if (x == 0.f) return x;
+    float r = (float)sqrt((double)x);
+    const float dn = nextafterf(r, 0.f), up = nextafterf(r, INFINITY);
+    const double lo = ((double)r + (double)dn) * 0.5, hi = ((double)r + (double)up) * 0.5;
+    const double xd = (double)x;
+    if (xd < lo * lo) r = dn;
+    else if (xd > hi * hi) r = up;
+    return r;
+}
+
+// Hashtable::get_median_count (src/oxli/hashtable.cc:299-328): one thread per
+// read; float32 in the reference's sequential order with round-to-nearest
+// intrinsics (no contraction), IEEE sqrt, median = sorted[n/2].
+__global__ void k_median(const uint64_t *koff, uint64_t nreads, uint16_t *counts, uint16_t *med, float *avg,
+                         float *sd) {
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < nreads;
+         r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t a = koff[r], n = koff[r + 1] - a;
+        uint16_t *c = counts + a;
+        float average = 0.f;
+        for (uint64_t t = 0; t < n; t++) average = __fadd_rn(average, (float)c[t]);
+        average = div_rn_exact(average, (float)n);
+        float s = 0.f;
+        for (uint64_t t = 0; t < n; t++) {
+            const float d = __fsub_rn((float)c[t], average);
+            s = __fadd_rn(s, __fmul_rn(d, d));
+        }
+        s = div_rn_exact(s, (float)n);
+        s = sqrt_rn_exact(s);
+        // in-place heapsort of the read's counts, then the middle element
+        uint64_t m = n;
+        auto sift = [&](uint64_t root, uint64_t end) {
+            while (2 * root + 1 < end) {
+                uint64_t child = 2 * root + 1;
+                if (child + 1 < end && c[child] < c[child + 1]) child++;
+                if (c[root] < c[child]) {
+                    uint16_t tmp = c[root]; c[root] = c[child]; c[child] = tmp;
+                    root = child;
+                } else {
+                    break;
+                }
+            }
+        };
+        for (uint64_t st = m / 2; st-- > 0;) sift(st, m);
+        for (uint64_t end = m; end-- > 1;) {
+            uint16_t tmp = c[0]; c[0] = c[end]; c[end] = tmp;
+            sift(0, end);
+        }
+        med[r] = c[n / 2];
+        avg[r] = average;
+        sd[r] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// batch boundaries of a device read set: chunk i starts at the last read whose
+// k-mer offset is <= koff[0] + i*B
+__global__ void k_chunk_bounds(const uint64_t *koff, uint64_t nreads, uint64_t B, uint64_t nchunks,
+                               uint64_t *out_r, uint64_t *out_k) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i <= nchunks;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t r;
+        if (i == nchunks) {
+            r = nreads;
+        } else {
+            const uint64_t target = koff[0] + i * B;
+            uint64_t lo = 0, hi = nreads;  // koff[lo] <= target
+            while (hi - lo > 1) {
+                uint64_t mid = (lo + hi) >> 1;
+                if (koff[mid] <= target) lo = mid; else hi = mid;
+            }
+            r = lo;
+        }
+        out_r[i] = r;
+        out_k[i] = koff[r];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic reads straight into HBM (khmer_amd/synth.py defines the stream):
+// word t of read r = mix(seed + (r * 2^20 + t) * golden)
+__device__ __forceinline__ uint64_t synth_word(uint64_t seed, uint64_t r, uint64_t t) {
+    uint64_t z = seed + ((r << 20) + t) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void k_synth_packed(uint64_t seed, uint64_t r0, uint64_t nreads, int L, int k, uint64_t *words,
+                               uint64_t nwords, uint64_t *koff) {
+    const uint64_t nbases = nreads * (uint64_t)L;
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nwords;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t out = 0;
+        uint64_t last_key = ~0ull, src = 0;
+        for (int b = 0; b < 32; b++) {
+            const uint64_t p = w * 32 + b;
+            uint64_t code = 0;
+            if (p < nbases) {
+                const uint64_t r = p / (uint64_t)L, i = p % (uint64_t)L;
+                const uint64_t key = (r << 20) | (i >> 5);
+                if (key != last_key) { src = synth_word(seed, r0 + r, i >> 5); last_key = key; }
+                code = (src >> (62 - 2 * (i & 31))) & 3;
+            }
+            out = (out << 2) | code;
+        }
+        words[w] = out;
+    }
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r <= nreads;
+         r += (uint64_t)gridDim.x * blockDim.x)
+        koff[r] = r * (uint64_t)(L - k + 1);
+}
+
+}  // namespace kh

@@ -1,0 +1,144 @@
+// kh_src.cuh -- k-mer sources of a device batch (included by kh_engine.hip).
+//
+// A batch is a sub-range of a read set.  Batch-local k-mer j is absolute k-mer
+// kbase + j; the base of read r in the packed stream is koff[r] + r*(k-1)
+// (reads are packed back to back, every read holds >= 1 k-mer).
+//   * fixed-length reads (kpr = k-mers per read != 0): the read of absolute
+//     k-mer ja is ja / kpr (Barrett), no offset array is touched;
+//   * variable-length reads: an LDS window of the batch's k-mer offsets per
+//     tile and a binary search in LDS.
+#pragma once
+#include "kh_internal.h"
+
+namespace kh {
+
+__device__ __forceinline__ uint64_t div_barrett(uint64_t x, uint64_t d, uint64_t m) {
+    uint64_t q = umulhi64(x, m);
+    return (x - q * d >= d) ? q + 1 : q;
+}
+
+struct SrcCommon {
+    const uint64_t *koff;   // offsets of this batch's reads (absolute values); unused when kpr != 0
+    uint64_t nreads;        // reads in this batch (variable-length mode)
+    uint64_t kbase;         // absolute index of batch k-mer 0
+    uint64_t rbase;         // absolute index of koff[0]'s read
+    uint64_t kpr, kpr_m;    // fixed k-mers per read and its Barrett constant (0 = variable)
+    int k;
+};
+
+struct SrcTwoBit : SrcCommon {
+    const uint64_t *words;
+    static constexpr bool kReads = true;
+    __device__ __forceinline__ uint64_t at(uint64_t ja, uint64_t r) const {
+        return canonical2(window2(words, ja + r * (uint64_t)(k - 1), k), k);
+    }
+};
+
+struct SrcBytes : SrcCommon {
+    const uint8_t *bytes;
+    static constexpr bool kReads = true;
+    __device__ __forceinline__ uint64_t at(uint64_t ja, uint64_t r) const {
+        return murmur_canonical(bytes + ja + r * (uint64_t)(k - 1), k);
+    }
+};
+
+struct SrcHashes : SrcCommon {
+    const uint64_t *h;
+    static constexpr bool kReads = false;
+    __device__ __forceinline__ uint64_t at(uint64_t ja, uint64_t) const { return h[ja - kbase]; }
+};
+
+// LDS window of read offsets covering k-mer tile [j0, j1) (variable mode)
+struct TileReads {
+    uint64_t rlo;
+    uint32_t n;
+};
+
+template <class Src>
+__device__ __forceinline__ bool needs_window(const Src &src) {
+    if constexpr (!Src::kReads) return false;
+    else return src.kpr == 0;
+}
+
+// All threads of the block must call this (it synchronises when a window is
+// needed; the caller must __syncthreads() itself otherwise).
+template <class Src>
+__device__ __forceinline__ TileReads load_tile_reads(const Src &src, uint64_t j0, uint64_t j1,
+                                                     uint64_t *s_koff, uint64_t *s_meta) {
+    TileReads tr{0, 0};
+    if (!needs_window(src)) return tr;
+    if (threadIdx.x == 0) {
+        const uint64_t ja = j0 + src.kbase;
+        uint64_t lo = 0, hi = src.nreads;  // koff[lo] <= ja < koff[hi]
+        while (hi - lo > 1) {
+            uint64_t mid = (lo + hi) >> 1;
+            if (src.koff[mid] <= ja) lo = mid; else hi = mid;
+        }
+        uint64_t cnt = src.nreads - lo;
+        if (cnt > j1 - j0) cnt = j1 - j0;
+        s_meta[0] = lo;
+        s_meta[1] = cnt;
+    }
+    __syncthreads();
+    tr.rlo = s_meta[0];
+    tr.n = (uint32_t)s_meta[1];
+    for (uint32_t t = threadIdx.x; t <= tr.n; t += blockDim.x) s_koff[t] = src.koff[tr.rlo + t];
+    __syncthreads();
+    return tr;
+}
+
+// hash of batch k-mer j inside a tile
+template <class Src>
+__device__ __forceinline__ uint64_t kmer_hash(const Src &src, const uint64_t *s_koff, const TileReads &tr,
+                                              uint64_t j) {
+    const uint64_t ja = j + src.kbase;
+    if constexpr (!Src::kReads) {
+        return src.at(ja, 0);
+    } else {
+        uint64_t r;
+        if (src.kpr) {
+            r = div_barrett(ja, src.kpr, src.kpr_m);
+        } else {
+            uint32_t lo = 0, hi = tr.n;
+            while (hi - lo > 1) {
+                uint32_t mid = (lo + hi) >> 1;
+                if (s_koff[mid] <= ja) lo = mid; else hi = mid;
+            }
+            r = src.rbase + tr.rlo + lo;
+        }
+        return src.at(ja, r);
+    }
+}
+
+// hash of batch k-mer j without a tile window (rare paths: bigcount, outputs)
+template <class Src>
+__device__ __forceinline__ uint64_t kmer_hash_global(const Src &src, uint64_t j) {
+    const uint64_t ja = j + src.kbase;
+    if constexpr (!Src::kReads) {
+        return src.at(ja, 0);
+    } else {
+        uint64_t r;
+        if (src.kpr) {
+            r = div_barrett(ja, src.kpr, src.kpr_m);
+        } else {
+            uint64_t lo = 0, hi = src.nreads;
+            while (hi - lo > 1) {
+                uint64_t mid = (lo + hi) >> 1;
+                if (src.koff[mid] <= ja) lo = mid; else hi = mid;
+            }
+            r = src.rbase + lo;
+        }
+        return src.at(ja, r);
+    }
+}
+
+__device__ __forceinline__ uint64_t global_bin(const Params &P, int i, uint64_t h) {
+    return P.tbase[i] + mod_barrett(h, P.p[i], P.m[i]);
+}
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+}  // namespace kh

@@ -221,3 +221,48 @@ def test_device_synth_matches_host_synth():
     o = O.Table(O.BYTE, k, sizes)
     o.consume_batch(seqs, [int(v) for v in offs])
     assert_same(g, o, "device synth")
+
+
+@pytest.mark.parametrize("fixed", [True, False])
+@pytest.mark.parametrize("batch", [1 << 20, 50000])
+def test_device_packed_paths_batched(fixed, batch):
+    """Fixed- and variable-length device paths, one and many device batches."""
+    import ctypes
+    from khmer_amd._lib import lib, check
+    n, L, k = 20000, 150, 21
+    sizes = O.get_n_primes_near_x(4, 1000003)
+    g = khmer.Countgraph(k, 1, 1, primes=sizes)
+    g.set_use_bigcount(True)
+    check(lib.kh_graph_set_batch_kmers(g._g, batch))
+    dev = khmer._lib.default_device()
+    w, ko = ctypes.c_void_p(), ctypes.c_void_p()
+    check(lib.kh_device_malloc(dev, (n * L // 32 + 2) * 8, ctypes.byref(w)))
+    check(lib.kh_device_malloc(dev, (n + 1) * 8, ctypes.byref(ko)))
+    check(lib.kh_synth_packed_device(dev, synth.SEED, 0, n, L, k, w, ko))
+    if fixed:
+        check(lib.kh_consume_packed_fixed_device(g._g, w, n, L))
+    else:
+        check(lib.kh_consume_packed_device(g._g, w, ko, n, n * (L - k + 1)))
+    lib.kh_device_free(dev, w)
+    lib.kh_device_free(dev, ko)
+    seqs, offs = synth.batch(0, n, L)
+    o = O.Table(O.BYTE, k, sizes)
+    o.set_use_bigcount(True)
+    o.consume_batch(seqs, [int(v) for v in offs])
+    assert_same(g, o, "device packed fixed=%s batch=%d" % (fixed, batch))
+
+
+def test_variable_length_reads_multi_batch(tmp_path):
+    """Ragged reads (1..300 bp) through several device batches."""
+    rng = np.random.default_rng(11)
+    path = str(tmp_path / "ragged.fa")
+    with open(path, "w") as fh:
+        for i in range(4000):
+            L = int(rng.integers(1, 300))
+            fh.write(">%d\n%s\n" % (i, "".join(rng.choice(list("ACGTN"), L))))
+    for cls in ("Countgraph", "Nodegraph", "SmallCountgraph"):
+        g, o = make_pair(cls, 25, O.get_n_primes_near_x(3, 300007), bigcount=(cls == "Countgraph"))
+        from khmer_amd._lib import lib
+        lib.kh_graph_set_batch_kmers(g._g, 20000)
+        assert g.consume_seqfile(path) == o.consume_fastx(path)
+        assert_same(g, o, "ragged " + cls)
