@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("-x", type=float, default=1e9)
     ap.add_argument("--batch-kmers", type=int, default=1 << 28)
     ap.add_argument("--no-bigcount", action="store_true")
+    ap.add_argument("--ablate", type=int, default=0,
+                    help="timing-only KH_ABLATE bits (results become wrong; never for reported numbers)")
     ap.add_argument("--variable-path", action="store_true",
                     help="feed k-mer offsets (variable-length read path) instead of the fixed-length path")
     ap.add_argument("--cpu-reads", type=int, default=1_000_000,
@@ -93,6 +95,8 @@ def cpu_baseline(args, sizes):
 
 def main():
     args = parse()
+    if args.ablate:
+        os.environ["KH_ABLATE"] = str(args.ablate)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

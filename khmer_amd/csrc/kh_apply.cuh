@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 2) k_apply_count(Params P, Appl
         for (uint32_t t = threadIdx.x; t < R / 512; t += blockDim.x) chg[t] = 0;
         __syncthreads();
         // records: four independent loads in flight per thread
-        for (uint64_t q0 = e0 + threadIdx.x; q0 < e1; q0 += 4ull * blockDim.x) {
+        for (uint64_t q0 = e0 + threadIdx.x; q0 < (P.ablate & 2 ? e0 : e1); q0 += 4ull * blockDim.x) {
             uint64_t v[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 2) k_apply_count(Params P, Appl
             if (!n) continue;
             const uint32_t c = c0[o];
             if (c == 0) {
-                A.newf[minj[o]] = 1;
+                if (!(P.ablate & 1)) A.newf[minj[o]] = 1;
                 occ += (i == 0);
             }
             const uint32_t v = c + n;
@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 2) k_apply_count(Params P, Appl
         __syncthreads();
         // pass 2: write back changed 16-bin chunks
         for (uint32_t t = threadIdx.x; t < nchunk; t += blockDim.x) {
-            if (!((chg[t >> 5] >> (t & 31)) & 1)) continue;
+            if (!((chg[t >> 5] >> (t & 31)) & 1) || (P.ablate & 4)) continue;
             const uint4 cv = ((const uint4 *)c0)[t];
             if (KIND == BYTE) {
                 ((uint4 *)(tab + bin_lo))[t] = cv;

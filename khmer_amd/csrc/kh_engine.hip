@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -530,6 +531,10 @@ void graph_prepare_params(Graph *g) {
     P.k = g->k;
     P.n = g->n;
     P.use_bigcount = g->use_bigcount ? 1 : 0;
+    // KH_ABLATE: timing-only switches that skip work (wrong results); bench
+    // ablation studies only
+    const char *ab = getenv("KH_ABLATE");
+    P.ablate = ab ? atoi(ab) : 0;
     P.s0 = g->kind == BIT ? 14 : 13;
     uint64_t maxreg = 1;
     for (int i = 0; i < g->n; i++) maxreg = std::max<uint64_t>(maxreg, (g->sizes[i] + (1ull << P.s0) - 1) >> P.s0);

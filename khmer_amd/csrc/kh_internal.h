@@ -54,6 +54,7 @@ struct Params {
     int s0, s2;
     uint32_t F1;
     int use_bigcount;
+    int ablate;               // timing-only ablation bits (KH_ABLATE env); 0 in normal use
     uint64_t p[MAXT];         // table sizes (bins)
     uint64_t m[MAXT];         // Barrett constants
     uint64_t tbase[MAXT];     // global bin base of table i

@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
     }
     __syncthreads();
     // pass C: coalesced runs
-    const uint32_t nrec = (uint32_t)((j1 - j0) * (uint64_t)nt);
+    const uint32_t nrec = (P.ablate & 8) ? 0 : (uint32_t)((j1 - j0) * (uint64_t)nt);
     for (uint32_t q = threadIdx.x; q < nrec; q += blockDim.x) {
         const uint32_t b = sb[q];
         rec[gbase[b] + (q - lstart[b])] = stage[q];
