@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("-k", type=int, default=21)
     ap.add_argument("--tables", type=int, default=4)
     ap.add_argument("-x", type=float, default=1e9)
-    ap.add_argument("--batch-kmers", type=int, default=1 << 28)
+    ap.add_argument("--batch-kmers", type=int, default=1 << 30)
     ap.add_argument("--no-bigcount", action="store_true")
     ap.add_argument("--ablate", type=int, default=0,
                     help="timing-only KH_ABLATE bits (results become wrong; never for reported numbers)")

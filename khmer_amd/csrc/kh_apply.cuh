@@ -1,25 +1,32 @@
-// kh_apply.cuh -- region apply, bigcount crossing resolution, finalize.
-// Included by kh_engine.hip.
+// kh_apply.cuh -- region apply, winner lists, bigcount crossing resolution,
+// finalize.  Included by kh_engine.hip.
 //
 // One workgroup owns one region of 2^s0 bins of one table at a time: the
-// table slice is read into LDS with 16-byte loads, every record of the region
-// bumps its bin's LDS counter and (for bins that were zero before the batch)
-// takes the minimum k-mer index (= the first insert in stream order, i.e. the
-// reference's is_new winner, storage.hh:578-588), then the saturated values
-// are written back with 16-byte stores.
+// table slice is held in LDS, every record of the region bumps its bin's LDS
+// counter and (for bins that were zero before the batch) takes the minimum
+// k-mer index (= the first insert in stream order, i.e. the reference's
+// is_new winner, storage.hh:578-588); the saturated values are written back
+// with 16-byte stores, and the winners are written to the region's own
+// segment of the winner list (win[e0 .. e0 + wcnt[rr])), so no global atomics
+// are needed.  The next region's table slice and first records are loaded
+// into registers while the current region finishes (software pipelining).
 #pragma once
 #include "kh_partition.cuh"
 
 namespace kh {
 
-constexpr int APPLY_THREADS = 1024;
+constexpr int APPLY_THREADS = 512;
+constexpr int APPLY_RECS = 8;          // records in flight per thread
 constexpr int FIN_THREADS = 256;
+constexpr int W_RPC = 64;              // regions per winner chunk
 
 struct ApplyArgs {
     const uint64_t *off2;
     const uint64_t *rec;
     uint8_t *tab;
-    uint8_t *newf, *fullf;
+    uint32_t *win;        // winners of region rr at win[e0(rr) ...]
+    uint32_t *wcnt;       // [regions] winners per region
+    uint8_t *fullf;
     uint64_t *cross;
     uint64_t cap_cross;
     uint64_t *ctr;
@@ -30,47 +37,139 @@ __device__ __forceinline__ void full_add(uint8_t *fullf, uint32_t j) {
     atomicAdd((uint32_t *)(fullf + (j & ~3u)), 1u << (8 * (j & 3u)));
 }
 
-__device__ __forceinline__ int region_table(const ApplyArgs &A, int n, uint64_t rr) {
+struct RegionInfo {
+    int i;
+    uint32_t nb;
+    uint64_t e0, e1, bin_lo;
+};
+
+// region rr (in apply order: table by table) -> table, bins, record range
+__device__ __forceinline__ RegionInfo region_info(const Params &P, const ApplyArgs &A, uint64_t rr) {
+    RegionInfo ri;
     int i = 0;
-    while (i + 1 < n && rr >= A.rprefix[i + 1]) i++;
-    return i;
+    while (i + 1 < P.n && rr >= A.rprefix[i + 1]) i++;
+    const uint64_t lreg = rr - A.rprefix[i];
+    const uint64_t region = (P.tbase[i] >> P.s0) + lreg;
+    ri.i = i;
+    ri.e0 = A.off2[region];
+    ri.e1 = A.off2[region + 1];
+    ri.bin_lo = lreg << P.s0;
+    ri.nb = (uint32_t)min((uint64_t)1 << P.s0, P.p[i] - ri.bin_lo);
+    return ri;
+}
+
+// registers prefetched for one region
+struct Prefetch {
+    RegionInfo ri;
+    uint4 tv;                   // this thread's 16-byte (8-byte nibble) table chunk
+    uint64_t v[APPLY_RECS];     // this thread's first records
+};
+
+template <int KIND>
+__device__ __forceinline__ void prefetch_region(const Params &P, const ApplyArgs &A, uint64_t rr, uint64_t total,
+                                                Prefetch &f) {
+    // every field is written on every path (keeps the struct in registers)
+    const bool valid = rr < total;
+    f.ri = region_info(P, A, valid ? rr : 0);
+    if (!valid) f.ri.e1 = f.ri.e0;
+    f.tv = make_uint4(0, 0, 0, 0);
+    const uint32_t t = threadIdx.x;
+    const bool any = f.ri.e0 != f.ri.e1;
+    const uint8_t *tab = A.tab + P.tbyte[f.ri.i];
+    if (KIND == BYTE) {
+        if (any && t < (f.ri.nb + 15) / 16) f.tv = ((const uint4 *)(tab + f.ri.bin_lo))[t];
+    } else if (KIND == NIBBLE) {
+        if (any && t < (f.ri.nb + 15) / 16) {
+            const uint2 x = ((const uint2 *)(tab + (f.ri.bin_lo >> 1)))[t];
+            f.tv = make_uint4(x.x, x.y, 0, 0);
+        }
+    } else {
+        if (any && t < (f.ri.nb + 127) / 128) f.tv = ((const uint4 *)(tab + (f.ri.bin_lo >> 3)))[t];
+    }
+#pragma unroll
+    for (int u = 0; u < APPLY_RECS; u++) {
+        const uint64_t q = f.ri.e0 + (uint64_t)u * APPLY_THREADS + t;
+        f.v[u] = q < f.ri.e1 ? A.rec[q] : ~0ull;
+    }
+}
+
+// one record of a Byte/Nibble region: two independent fire-and-forget LDS
+// atomics (no dependence on the bin's value, so loads and atomics pipeline)
+__device__ __forceinline__ void count_record(uint64_t x, uint32_t *cnt, uint32_t *minj) {
+    if (x == ~0ull) return;
+    const uint32_t o = (uint32_t)x;
+    atomicAdd(&cnt[o], 1u);
+    atomicMin(&minj[o], (uint32_t)(x >> 32));
+}
+// one record of a Bit region
+__device__ __forceinline__ void bit_record(uint64_t x, uint32_t *minj) {
+    if (x == ~0ull) return;
+    atomicMin(&minj[(uint32_t)x], (uint32_t)(x >> 32));
+}
+
+// winners (held in registers) -> the region's segment of the winner list.
+// Called by all threads after a barrier that follows wave_winner_scan.
+__device__ __forceinline__ uint32_t wave_winner_scan(uint32_t c, uint32_t *s_wt) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t incl = c;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+    }
+    if (lane == 63) s_wt[threadIdx.x >> 6] = incl;
+    return incl - c;
+}
+__device__ __forceinline__ uint64_t winner_base(const uint32_t *s_wt, uint32_t *total) {
+    const uint32_t wave = threadIdx.x >> 6, nwav = blockDim.x >> 6;
+    uint32_t before = 0, all = 0;
+    for (uint32_t w = 0; w < nwav; w++) {
+        const uint32_t x = s_wt[w];
+        before += w < wave ? x : 0;
+        all += x;
+    }
+    *total = all;
+    return before;
 }
 
 // Byte (KIND == BYTE) and Nibble storage: ByteStorage::add / NibbleStorage::add
 // (storage.hh:571-624 / 320-359) applied as a batch
 template <int KIND>
-__global__ void __launch_bounds__(APPLY_THREADS, 2) k_apply_count(Params P, ApplyArgs A) {
+__global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, ApplyArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int BPT = 16;               // 2^13 bins / 512 threads
     const uint32_t R = 1u << P.s0;
     uint32_t *cnt = (uint32_t *)smem;     // [R]
     uint32_t *minj = cnt + R;             // [R]
     uint32_t *chg = minj + R;             // [R/512] changed 16-bin chunks
-    uint8_t *c0 = (uint8_t *)(chg + R / 512);  // [R]
+    uint32_t *s_wt = chg + R / 512;       // [16] wave winner totals
+    uint32_t *full255 = s_wt + 16;        // [R/32] bins at 255 before the batch that got inserts
+    uint32_t *s_flag = full255 + R / 32;  // [4]
+    uint8_t *c0 = (uint8_t *)(s_flag + 4);  // [R]
     const uint32_t MAXC = KIND == BYTE ? 255u : 15u;
     const bool bigc = KIND == BYTE && P.use_bigcount;
+    const uint32_t t = threadIdx.x;
     uint64_t occ = 0;
     const uint64_t total = A.rprefix[P.n];
+    Prefetch cur, nxt;
+    prefetch_region<KIND>(P, A, blockIdx.x, total, cur);
     for (uint64_t rr = blockIdx.x; rr < total; rr += gridDim.x) {
-        const int i = region_table(A, P.n, rr);
-        const uint64_t lreg = rr - A.rprefix[i];
-        const uint64_t region = (P.tbase[i] >> P.s0) + lreg;
-        const uint64_t e0 = A.off2[region], e1 = A.off2[region + 1];
-        if (e0 == e1) continue;
-        const uint64_t bin_lo = lreg << P.s0;
-        const uint32_t nb = (uint32_t)min((uint64_t)R, P.p[i] - bin_lo);
-        const uint32_t nchunk = (nb + 15) / 16;   // 16 bins per thread-chunk
-        uint8_t *tab = A.tab + P.tbyte[i];
-        // table slice -> LDS (16-byte loads; the arena pads every table to 256 B)
-        if (KIND == BYTE) {
-            const uint4 *src = (const uint4 *)(tab + bin_lo);
-            for (uint32_t t = threadIdx.x; t < nchunk; t += blockDim.x) ((uint4 *)c0)[t] = src[t];
-        } else {
-            const uint2 *src = (const uint2 *)(tab + (bin_lo >> 1));
-            for (uint32_t t = threadIdx.x; t < nchunk; t += blockDim.x) {
-                const uint2 v = src[t];
+        const RegionInfo ri = cur.ri;
+        if (ri.e0 == ri.e1) {
+            if (t == 0) A.wcnt[rr] = 0;
+            prefetch_region<KIND>(P, A, rr + gridDim.x, total, cur);
+            continue;
+        }
+        const uint32_t nb = ri.nb;
+        const uint32_t nchunk = (nb + 15) / 16;   // 16 bins per chunk
+        uint8_t *tab = A.tab + P.tbyte[ri.i];
+        // table chunk (registers) -> LDS; counters and winners reset
+        if (t < nchunk) {
+            if (KIND == BYTE) {
+                ((uint4 *)c0)[t] = cur.tv;
+            } else {
                 uint4 o;
                 uint32_t *ow = (uint32_t *)&o;
-                const uint32_t w[2] = {v.x, v.y};
+                const uint32_t w[2] = {cur.tv.x, cur.tv.y};
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
 #pragma unroll
@@ -83,46 +182,60 @@ __global__ void __launch_bounds__(APPLY_THREADS, 2) k_apply_count(Params P, Appl
                 ((uint4 *)c0)[t] = o;
             }
         }
-        for (uint32_t t = threadIdx.x; t < nchunk * 4; t += blockDim.x) {
-            ((uint4 *)cnt)[t] = make_uint4(0, 0, 0, 0);
-            ((uint4 *)minj)[t] = make_uint4(NO_J, NO_J, NO_J, NO_J);
+        for (uint32_t x = t; x < nchunk * 4; x += blockDim.x) {
+            ((uint4 *)cnt)[x] = make_uint4(0, 0, 0, 0);
+            ((uint4 *)minj)[x] = make_uint4(NO_J, NO_J, NO_J, NO_J);
         }
-        for (uint32_t t = threadIdx.x; t < R / 512; t += blockDim.x) chg[t] = 0;
-        __syncthreads();
-        // records: four independent loads in flight per thread
-        for (uint64_t q0 = e0 + threadIdx.x; q0 < (P.ablate & 2 ? e0 : e1); q0 += 4ull * blockDim.x) {
-            uint64_t v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint64_t q = q0 + (uint64_t)u * blockDim.x;
-                v[u] = q < e1 ? A.rec[q] : ~0ull;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (v[u] == ~0ull) continue;
-                const uint32_t o = (uint32_t)v[u];
-                const uint32_t j = (uint32_t)(v[u] >> 32);
-                atomicAdd(&cnt[o], 1u);
-                const uint8_t c = c0[o];
-                if (c == 0) atomicMin(&minj[o], j);
-                if (bigc && c == 255) full_add(A.fullf, j);
-            }
+        if (t < R / 512) chg[t] = 0;
+        if (bigc) {
+            for (uint32_t x = t; x < R / 32; x += blockDim.x) full255[x] = 0;
+            if (t == 0) s_flag[0] = 0;
         }
         __syncthreads();
-        // pass 1 (thread per bin, conflict-free LDS): winners, crossings,
-        // saturated value into c0, changed-chunk bitmap
-        for (uint32_t o = threadIdx.x; o < nb; o += blockDim.x) {
+        // records: the prefetched batch, then APPLY_RECS loads in flight per thread
+        if (!(P.ablate & 2)) {
+#pragma unroll
+            for (int u = 0; u < APPLY_RECS; u++) count_record(cur.v[u], cnt, minj);
+            const uint64_t step = (uint64_t)APPLY_RECS * APPLY_THREADS;
+            for (uint64_t q0 = ri.e0 + step + t; q0 < ri.e1; q0 += step) {
+                uint64_t v[APPLY_RECS];
+#pragma unroll
+                for (int u = 0; u < APPLY_RECS; u++) {
+                    const uint64_t q = q0 + (uint64_t)u * APPLY_THREADS;
+                    v[u] = q < ri.e1 ? A.rec[q] : ~0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < APPLY_RECS; u++) count_record(v[u], cnt, minj);
+            }
+        }
+        __syncthreads();
+        prefetch_region<KIND>(P, A, rr + gridDim.x, total, nxt);
+        // pass 1 (thread per bin, conflict-free LDS): winners (bins zero
+        // before the batch keep their minimum k-mer index, the others drop
+        // it), crossings, bins already full, saturated value into c0, changed
+        // chunks
+        uint32_t nw = 0;
+#pragma unroll 2
+        for (int u = 0; u < BPT; u++) {
+            const uint32_t o = t + (uint32_t)u * APPLY_THREADS;
+            if (o >= nb) continue;
             const uint32_t n = cnt[o];
             if (!n) continue;
             const uint32_t c = c0[o];
             if (c == 0) {
-                if (!(P.ablate & 1)) A.newf[minj[o]] = 1;
-                occ += (i == 0);
+                nw++;
+                occ += (ri.i == 0);
+            } else {
+                minj[o] = NO_J;
+            }
+            if (bigc && c == 255) {
+                atomicOr(&full255[o >> 5], 1u << (o & 31));
+                s_flag[0] = 1;
             }
             const uint32_t v = c + n;
             if (bigc && c < 255 && v >= 255) {
                 const uint64_t idx = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
-                if (idx < A.cap_cross) A.cross[idx] = ((P.tbase[i] + bin_lo + o) << 8) | c;
+                if (idx < A.cap_cross) A.cross[idx] = ((P.tbase[ri.i] + ri.bin_lo + o) << 8) | c;
                 else atomicOr((unsigned long long *)&A.ctr[CTR_ERR], 1ull);
             }
             const uint32_t f = v < MAXC ? v : MAXC;
@@ -131,13 +244,15 @@ __global__ void __launch_bounds__(APPLY_THREADS, 2) k_apply_count(Params P, Appl
                 atomicOr(&chg[o >> 9], 1u << ((o >> 4) & 31));
             }
         }
+        if (P.ablate & 1) nw = 0;
+        const uint32_t wex = wave_winner_scan(nw, s_wt);
         __syncthreads();
-        // pass 2: write back changed 16-bin chunks
-        for (uint32_t t = threadIdx.x; t < nchunk; t += blockDim.x) {
-            if (!((chg[t >> 5] >> (t & 31)) & 1) || (P.ablate & 4)) continue;
-            const uint4 cv = ((const uint4 *)c0)[t];
+        // pass 2: write back changed 16-bin chunks; winners to the region's segment
+        for (uint32_t x = t; x < nchunk; x += blockDim.x) {
+            if (!((chg[x >> 5] >> (x & 31)) & 1) || (P.ablate & 4)) continue;
+            const uint4 cv = ((const uint4 *)c0)[x];
             if (KIND == BYTE) {
-                ((uint4 *)(tab + bin_lo))[t] = cv;
+                ((uint4 *)(tab + ri.bin_lo))[x] = cv;
             } else {
                 // even bin -> high nibble (storage.hh:262-272)
                 const uint8_t *fin = (const uint8_t *)&cv;
@@ -151,72 +266,234 @@ __global__ void __launch_bounds__(APPLY_THREADS, 2) k_apply_count(Params P, Appl
                         w |= (uint32_t)((fin[8 * h + 2 * b] << 4) | fin[8 * h + 2 * b + 1]) << (8 * b);
                     ow[h] = w;
                 }
-                ((uint2 *)(tab + (bin_lo >> 1)))[t] = o;
+                ((uint2 *)(tab + (ri.bin_lo >> 1)))[x] = o;
             }
         }
+        if (bigc && s_flag[0]) {
+            // bins at 255 before the batch: every insert is "full"
+            // (ByteStorage::add, storage.hh:590-603); rare, so the region's
+            // records are read again
+            for (uint64_t q = ri.e0 + t; q < ri.e1; q += APPLY_THREADS) {
+                const uint64_t x = A.rec[q];
+                const uint32_t o = (uint32_t)x;
+                if ((full255[o >> 5] >> (o & 31)) & 1) full_add(A.fullf, (uint32_t)(x >> 32));
+            }
+        }
+        uint32_t wall;
+        uint64_t pos = ri.e0 + winner_base(s_wt, &wall) + wex;
+        if (nw) {
+#pragma unroll 2
+            for (int u = 0; u < BPT; u++) {
+                const uint32_t o = t + (uint32_t)u * APPLY_THREADS;
+                const uint32_t m = o < nb ? minj[o] : NO_J;
+                if (m != NO_J) A.win[pos++] = m;
+            }
+        }
+        if (t == 0) A.wcnt[rr] = wall;
         __syncthreads();
+        cur = nxt;
     }
     occ = wave_sum(occ);
     if ((threadIdx.x & 63) == 0 && occ) atomicAdd((unsigned long long *)&A.ctr[CTR_OCC], (unsigned long long)occ);
 }
 
 // Bit storage (Bloom): BitStorage::test_and_set_bits (storage.hh:172-199)
-__global__ void __launch_bounds__(APPLY_THREADS, 2) k_apply_bit(Params P, ApplyArgs A) {
+__global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int BPT = 32;               // 2^14 bins / 512 threads
     const uint32_t R = 1u << P.s0;
     uint32_t *minj = (uint32_t *)smem;          // [R]
-    uint32_t *chg = minj + R;                   // [R/4096] changed 128-bin chunks
-    uint32_t *bits32 = chg + (R / 4096 < 4 ? 4 : R / 4096);  // [R/32]
+    uint32_t *chg = minj + R;                   // [4] changed 128-bin chunks
+    uint32_t *s_wt = chg + 4;                   // [16]
+    uint32_t *bits32 = s_wt + 16;               // [R/32]
     uint8_t *bits = (uint8_t *)bits32;
+    const uint32_t t = threadIdx.x;
     uint64_t occ = 0;
     const uint64_t total = A.rprefix[P.n];
+    Prefetch cur, nxt;
+    prefetch_region<BIT>(P, A, blockIdx.x, total, cur);
     for (uint64_t rr = blockIdx.x; rr < total; rr += gridDim.x) {
-        const int i = region_table(A, P.n, rr);
-        const uint64_t lreg = rr - A.rprefix[i];
-        const uint64_t region = (P.tbase[i] >> P.s0) + lreg;
-        const uint64_t e0 = A.off2[region], e1 = A.off2[region + 1];
-        if (e0 == e1) continue;
-        const uint64_t bin_lo = lreg << P.s0;
-        const uint32_t nb = (uint32_t)min((uint64_t)R, P.p[i] - bin_lo);
+        const RegionInfo ri = cur.ri;
+        if (ri.e0 == ri.e1) {
+            if (t == 0) A.wcnt[rr] = 0;
+            prefetch_region<BIT>(P, A, rr + gridDim.x, total, cur);
+            continue;
+        }
+        const uint32_t nb = ri.nb;
         const uint32_t nchunk = (nb + 127) / 128;   // 16 bytes = 128 bins per chunk
-        uint8_t *tab = A.tab + P.tbyte[i] + (bin_lo >> 3);
-        for (uint32_t t = threadIdx.x; t < nchunk; t += blockDim.x) ((uint4 *)bits)[t] = ((const uint4 *)tab)[t];
-        for (uint32_t t = threadIdx.x; t < nchunk * 32; t += blockDim.x)
-            ((uint4 *)minj)[t] = make_uint4(NO_J, NO_J, NO_J, NO_J);
-        for (uint32_t t = threadIdx.x; t < 4; t += blockDim.x) chg[t] = 0;
+        uint8_t *tab = A.tab + P.tbyte[ri.i] + (ri.bin_lo >> 3);
+        if (t < nchunk) ((uint4 *)bits)[t] = cur.tv;
+        for (uint32_t x = t; x < nchunk * 32; x += blockDim.x) ((uint4 *)minj)[x] = make_uint4(NO_J, NO_J, NO_J, NO_J);
+        if (t < 4) chg[t] = 0;
         __syncthreads();
-        for (uint64_t q0 = e0 + threadIdx.x; q0 < e1; q0 += 4ull * blockDim.x) {
-            uint64_t v[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint64_t q = q0 + (uint64_t)u * blockDim.x;
-                v[u] = q < e1 ? A.rec[q] : ~0ull;
+        for (int u = 0; u < APPLY_RECS; u++) bit_record(cur.v[u], minj);
+        const uint64_t step = (uint64_t)APPLY_RECS * APPLY_THREADS;
+        for (uint64_t q0 = ri.e0 + step + t; q0 < ri.e1; q0 += step) {
+            uint64_t v[APPLY_RECS];
+#pragma unroll
+            for (int u = 0; u < APPLY_RECS; u++) {
+                const uint64_t q = q0 + (uint64_t)u * APPLY_THREADS;
+                v[u] = q < ri.e1 ? A.rec[q] : ~0ull;
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (v[u] == ~0ull) continue;
-                const uint32_t o = (uint32_t)v[u];
-                if (!((bits[o >> 3] >> (o & 7)) & 1)) atomicMin(&minj[o], (uint32_t)(v[u] >> 32));
-            }
+            for (int u = 0; u < APPLY_RECS; u++) bit_record(v[u], minj);
         }
         __syncthreads();
+        prefetch_region<BIT>(P, A, rr + gridDim.x, total, nxt);
         // pass 1 (thread per bin): winners set their bit
-        for (uint32_t o = threadIdx.x; o < nb; o += blockDim.x) {
-            const uint32_t mj = minj[o];
-            if (mj == NO_J) continue;
+        uint32_t nw = 0;
+#pragma unroll 2
+        for (int u = 0; u < BPT; u++) {
+            const uint32_t o = t + (uint32_t)u * APPLY_THREADS;
+            if (o >= nb || minj[o] == NO_J) continue;
+            if ((bits[o >> 3] >> (o & 7)) & 1) {   // bit already set: not new
+                minj[o] = NO_J;
+                continue;
+            }
             atomicOr(&bits32[o >> 5], 1u << (o & 31));
             atomicOr(&chg[o >> 12], 1u << ((o >> 7) & 31));
-            A.newf[mj] = 1;
-            occ += (i == 0);
+            nw++;
+            occ += (ri.i == 0);
         }
+        const uint32_t wex = wave_winner_scan(nw, s_wt);
         __syncthreads();
-        // pass 2: write back changed 128-bin chunks
-        for (uint32_t t = threadIdx.x; t < nchunk; t += blockDim.x)
-            if ((chg[t >> 5] >> (t & 31)) & 1) ((uint4 *)tab)[t] = ((const uint4 *)bits)[t];
+        // pass 2: write back changed 128-bin chunks; winners
+        for (uint32_t x = t; x < nchunk; x += blockDim.x)
+            if ((chg[x >> 5] >> (x & 31)) & 1) ((uint4 *)tab)[x] = ((const uint4 *)bits)[x];
+        uint32_t wall;
+        uint64_t pos = ri.e0 + winner_base(s_wt, &wall) + wex;
+        if (nw) {
+#pragma unroll 2
+            for (int u = 0; u < BPT; u++) {
+                const uint32_t o = t + (uint32_t)u * APPLY_THREADS;
+                const uint32_t m = o < nb ? minj[o] : NO_J;
+                if (m != NO_J) A.win[pos++] = m;
+            }
+        }
+        if (t == 0) A.wcnt[rr] = wall;
         __syncthreads();
+        cur = nxt;
     }
     occ = wave_sum(occ);
     if ((threadIdx.x & 63) == 0 && occ) atomicAdd((unsigned long long *)&A.ctr[CTR_OCC], (unsigned long long)occ);
+}
+
+// ---------------------------------------------------------------------------
+// winner lists -> k-mer windows of 2^js (chunks of W_RPC consecutive regions)
+__device__ __forceinline__ uint32_t w_chunk_setup(const Params &P, const ApplyArgs &A, uint64_t total,
+                                                  uint32_t *s_pre, uint64_t *s_e0) {
+    const uint64_t rr0 = (uint64_t)blockIdx.x * W_RPC;
+    if (threadIdx.x < W_RPC) {
+        const uint64_t rr = rr0 + threadIdx.x;
+        const uint32_t c = rr < total ? A.wcnt[rr] : 0;
+        s_e0[threadIdx.x] = c ? region_info(P, A, rr).e0 : 0;
+        const uint32_t lane = threadIdx.x;
+        uint32_t incl = c;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= (uint32_t)d) incl += y;
+        }
+        s_pre[lane + 1] = incl;
+        if (lane == 0) s_pre[0] = 0;
+    }
+    __syncthreads();
+    return s_pre[W_RPC];
+}
+__device__ __forceinline__ uint32_t w_elem(const ApplyArgs &A, const uint32_t *s_pre, const uint64_t *s_e0,
+                                           uint32_t i) {
+    uint32_t lo = 0, hi = W_RPC;   // largest lo with s_pre[lo] <= i
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_pre[mid] <= i) lo = mid; else hi = mid;
+    }
+    return A.win[s_e0[lo] + (i - s_pre[lo])];
+}
+
+__global__ void __launch_bounds__(PT_THREADS) k_hist_w(Params P, ApplyArgs A, int js, uint32_t FJ, uint32_t nchw,
+                                                      uint32_t *M3) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *s_e0 = (uint64_t *)smem;             // [W_RPC]
+    uint32_t *s_pre = (uint32_t *)(s_e0 + W_RPC);  // [W_RPC + 1]
+    uint32_t *hist = s_pre + W_RPC + 4;            // [FJ]
+    for (uint32_t b = threadIdx.x; b < FJ; b += blockDim.x) hist[b] = 0;
+    const uint32_t n = w_chunk_setup(P, A, A.rprefix[P.n], s_pre, s_e0);
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[w_elem(A, s_pre, s_e0, i) >> js], 1u);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < FJ; b += blockDim.x) M3[(uint64_t)b * nchw + blockIdx.x] = hist[b];
+}
+
+__global__ void __launch_bounds__(PT_THREADS) k_scatter_w(Params P, ApplyArgs A, int js, uint32_t FJ, uint32_t nchw,
+                                                         const uint64_t *O3, uint32_t *wout) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t FJa = (FJ + 3) & ~3u;
+    uint64_t *s_e0 = (uint64_t *)smem;             // [W_RPC]
+    uint32_t *s_pre = (uint32_t *)(s_e0 + W_RPC);  // [W_RPC + 1]
+    uint64_t *lcur = (uint64_t *)(s_pre + W_RPC + 4);  // [FJ]  (W_RPC + 4 keeps 8-B alignment)
+    uint32_t *stage = (uint32_t *)(lcur + FJa);    // [PT_TILE]
+    uint32_t *tail = stage + PT_TILE;              // [FJ*8]
+    uint32_t *hist = tail + FJa * 8;               // [FJ]
+    uint32_t *lstart = hist + FJa;                 // [FJ]
+    uint8_t *hskip = (uint8_t *)(lstart + FJa);    // [FJ]
+    const Emit<uint32_t, 8, true> em{lcur, hskip, tail, hist, lstart};
+    for (uint32_t b = threadIdx.x; b < FJ; b += blockDim.x) em.init(b, O3[(uint64_t)b * nchw + blockIdx.x]);
+    const uint32_t n = w_chunk_setup(P, A, A.rprefix[P.n], s_pre, s_e0);
+    for (uint32_t t0 = 0; t0 < n; t0 += PT_TILE) {
+        const uint32_t t1 = min(n, t0 + PT_TILE);
+        const bool last = t1 == n;
+        __syncthreads();
+        uint32_t v[PT_RPT], rank[PT_RPT];
+#pragma unroll
+        for (int q = 0; q < PT_RPT; q++) {
+            const uint32_t idx = t0 + (uint32_t)q * PT_THREADS + threadIdx.x;
+            v[q] = idx < t1 ? w_elem(A, s_pre, s_e0, idx) : NO_J;
+        }
+#pragma unroll
+        for (int q = 0; q < PT_RPT; q++)
+            if (v[q] != NO_J) rank[q] = atomicAdd(&hist[v[q] >> js], 1u);
+        __syncthreads();
+        wave_exclusive_scan(hist, lstart, FJ);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PT_RPT; q++)
+            if (v[q] != NO_J) stage[lstart[v[q] >> js] + rank[q]] = v[q];
+        em.flush_tails(FJ, last, wout);
+        __syncthreads();
+        const uint32_t nrec = t1 - t0;
+        for (uint32_t q = threadIdx.x; q < nrec; q += blockDim.x) em.put(stage[q] >> js, q, stage[q], last, wout);
+        __syncthreads();
+        em.advance(FJ, last);
+    }
+}
+
+// one workgroup per window: bitmap of the window's winners in LDS; n_unique +=
+// its population; optionally the bitmap is written out (per-k-mer new flags)
+__global__ void __launch_bounds__(PT_THREADS) k_mark(const uint32_t *wout, const uint64_t *O3, const uint32_t *M3,
+                                                    uint32_t nchw, uint32_t FJ, int js, uint64_t *ctr,
+                                                    uint32_t *newbits) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *bits = (uint32_t *)smem;   // [2^js / 32]
+    const uint32_t nw = 1u << (js - 5);
+    const uint32_t jb = blockIdx.x;
+    const uint64_t s = O3[(uint64_t)jb * nchw];
+    const uint64_t last = (uint64_t)FJ * nchw - 1;
+    const uint64_t e = jb + 1 < FJ ? O3[(uint64_t)(jb + 1) * nchw] : O3[last] + M3[last];
+    for (uint32_t t = threadIdx.x; t < nw / 4; t += blockDim.x) ((uint4 *)bits)[t] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    const uint32_t mask = (1u << js) - 1;
+    for (uint64_t q = s + threadIdx.x; q < e; q += blockDim.x) {
+        const uint32_t j = wout[q] & mask;
+        atomicOr(&bits[j >> 5], 1u << (j & 31));
+    }
+    __syncthreads();
+    uint64_t uniq = 0;
+    for (uint32_t t = threadIdx.x; t < nw / 4; t += blockDim.x) {
+        const uint4 x = ((const uint4 *)bits)[t];
+        uniq += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+        if (newbits) ((uint4 *)(newbits + (uint64_t)jb * nw))[t] = x;
+    }
+    uniq = wave_sum(uniq);
+    if ((threadIdx.x & 63) == 0 && uniq) atomicAdd((unsigned long long *)&ctr[CTR_UNIQUE], (unsigned long long)uniq);
 }
 
 // ---------------------------------------------------------------------------
@@ -276,19 +553,16 @@ __global__ void __launch_bounds__(256) k_crossing(Params P, const uint64_t *off2
 }
 
 // ---------------------------------------------------------------------------
-// finalize: n_unique += #new k-mers (16 flags per thread via 16-byte loads);
-// k-mers full in every table feed the bigcount map; optional per-k-mer hashes
+// finalize (bigcount and/or per-k-mer hash output only): k-mers full in every
+// table feed the bigcount map (16 flags per thread via 16-byte loads)
 template <class Src>
-__global__ void __launch_bounds__(FIN_THREADS) k_finalize(Params P, Src src, uint64_t nkmers, const uint8_t *newf,
-                                                         const uint8_t *fullf, uint64_t *ctr, uint64_t *bc,
-                                                         uint64_t cap_bc, uint64_t *out_hash) {
+__global__ void __launch_bounds__(FIN_THREADS) k_finalize(Params P, Src src, uint64_t nkmers, const uint8_t *fullf,
+                                                         uint64_t *ctr, uint64_t *bc, uint64_t cap_bc,
+                                                         uint64_t *out_hash) {
     const bool bigc = P.kind == BYTE && P.use_bigcount;
     const uint64_t nchunk = (nkmers + 15) / 16;
-    uint64_t uniq = 0;
     for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nchunk;
          c += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4 nv = ((const uint4 *)newf)[c];   // bytes are 0/1, zero past nkmers
-        uniq += __popc(nv.x) + __popc(nv.y) + __popc(nv.z) + __popc(nv.w);
         if (bigc) {
             const uint4 fv = ((const uint4 *)fullf)[c];
             if (fv.x | fv.y | fv.z | fv.w) {
@@ -310,8 +584,6 @@ __global__ void __launch_bounds__(FIN_THREADS) k_finalize(Params P, Src src, uin
             }
         }
     }
-    uniq = wave_sum(uniq);
-    if ((threadIdx.x & 63) == 0 && uniq) atomicAdd((unsigned long long *)&ctr[CTR_UNIQUE], (unsigned long long)uniq);
 }
 
 }  // namespace kh

@@ -23,6 +23,8 @@
 #include <cstring>
 #include <vector>
 
+#include <rocprim/device/device_scan.hpp>
+
 #include "kh_apply.cuh"
 #include "kh_internal.h"
 #include "kh_query.cuh"
@@ -40,21 +42,53 @@ static void ensure(void **p, uint64_t *cap, uint64_t need, size_t elem) {
     *cap = n;
 }
 
-static void ws_prepare(Graph *g, uint64_t nkmers) {
+
+static int ceil_log2(uint64_t x) {
+    int s = 0;
+    while ((1ull << s) < x) s++;
+    return s;
+}
+
+// geometry of one device pass (all partitions are chunked counting sorts)
+struct PassGeo {
+    uint64_t nkmers, recs;
+    uint32_t ck1, nch1;        // level-1 chunk (k-mers) and chunk count
+    uint64_t nch2max;          // level-2 chunk bound
+    int js;                    // winner window = 2^js k-mers
+    uint32_t FJ, nchw;         // windows, winner chunks (W_RPC regions each)
+    uint64_t regions;          // table regions (apply order)
+    uint64_t mcnt;             // count-matrix entries (max over the three sorts)
+};
+
+static PassGeo pass_geo(const Params &P, uint64_t nkmers) {
+    PassGeo q;
+    q.nkmers = nkmers;
+    q.recs = nkmers * (uint64_t)P.n;
+    q.ck1 = 32768u * ((P.F1 + 1023) / 1024);
+    q.nch1 = (uint32_t)((nkmers + q.ck1 - 1) / q.ck1);
+    q.nch2max = q.recs / L2_CHUNK + P.F1 + 1;
+    q.js = std::max(17, ceil_log2(nkmers) - 11);   // <= 2048 windows of <= 2^20 k-mers
+    q.FJ = (uint32_t)((nkmers + (1ull << q.js) - 1) >> q.js);
+    q.regions = 0;
+    for (int i = 0; i < P.n; i++) q.regions += (P.p[i] + (1ull << P.s0) - 1) >> P.s0;
+    q.nchw = (uint32_t)((q.regions + W_RPC - 1) / W_RPC);
+    const uint64_t F2 = 1ull << P.s2;
+    q.mcnt = std::max<uint64_t>({(uint64_t)P.F1 * q.nch1, F2 * q.nch2max, (uint64_t)q.FJ * q.nchw});
+    return q;
+}
+
+static void ws_prepare(Graph *g, const PassGeo &q) {
     Workspace &w = g->ws;
-    const uint64_t recs = nkmers * (uint64_t)g->n;
-    if (nkmers > w.cap_kmers) {
-        uint64_t cap = std::max<uint64_t>(nkmers, w.cap_kmers + w.cap_kmers / 2);
+    if (q.nkmers > w.cap_kmers) {
+        uint64_t cap = std::max<uint64_t>(q.nkmers, w.cap_kmers + w.cap_kmers / 2);
         cap = (cap + 15) & ~15ull;
-        if (w.newf) KH_HIP(hipFree(w.newf));
         if (w.fullf) KH_HIP(hipFree(w.fullf));
-        w.newf = w.fullf = nullptr;
-        KH_HIP(hipMalloc((void **)&w.newf, cap + 64));
+        w.fullf = nullptr;
         KH_HIP(hipMalloc((void **)&w.fullf, cap + 64));
         w.cap_kmers = cap;
     }
-    if (recs > w.cap_recs) {
-        uint64_t cap = std::max<uint64_t>(recs, w.cap_recs + w.cap_recs / 2);
+    if (q.recs > w.cap_recs) {
+        uint64_t cap = std::max<uint64_t>(q.recs, w.cap_recs + w.cap_recs / 2);
         for (uint64_t **pp : {&w.rec1, &w.rec2}) {
             if (*pp) KH_HIP(hipFree(*pp));
             *pp = nullptr;
@@ -62,19 +96,18 @@ static void ws_prepare(Graph *g, uint64_t nkmers) {
         }
         w.cap_recs = cap;
     }
+    ensure((void **)&w.mcnt, &w.cap_m, q.mcnt, 4);
+    ensure((void **)&w.moff, &w.cap_moff, q.mcnt, 8);
+    ensure((void **)&w.wcnt, &w.cap_wcnt, q.regions, 4);
+    ensure((void **)&w.newbits, &w.cap_newbits, ((uint64_t)q.FJ << q.js) / 32, 4);
     const uint64_t regions = (uint64_t)g->prm.F1 << g->prm.s2;
-    if (regions > w.cap_regions || !w.cnt1) {
-        for (void **pp : {(void **)&w.cnt1, (void **)&w.off1, (void **)&w.cur1, (void **)&w.tile1, (void **)&w.cnt2,
-                          (void **)&w.off2, (void **)&w.cur2})
+    if (regions > w.cap_regions || !w.off1) {
+        for (void **pp : {(void **)&w.off1, (void **)&w.ch2, (void **)&w.off2})
             if (*pp) { KH_HIP(hipFree(*pp)); *pp = nullptr; }
         const uint64_t F1 = g->prm.F1;
-        KH_HIP(hipMalloc((void **)&w.cnt1, F1 * 4 + 64));
         KH_HIP(hipMalloc((void **)&w.off1, (F1 + 1) * 8 + 64));
-        KH_HIP(hipMalloc((void **)&w.cur1, F1 * 8 + 64));
-        KH_HIP(hipMalloc((void **)&w.tile1, (F1 + 1) * 4 + 64));
-        KH_HIP(hipMalloc((void **)&w.cnt2, regions * 4 + 64));
+        KH_HIP(hipMalloc((void **)&w.ch2, (F1 + 1) * 4 + 64));
         KH_HIP(hipMalloc((void **)&w.off2, (regions + 1) * 8 + 64));
-        KH_HIP(hipMalloc((void **)&w.cur2, regions * 8 + 64));
         w.cap_regions = regions;
     }
     if (!w.ctr) {
@@ -89,6 +122,18 @@ static void ws_prepare(Graph *g, uint64_t nkmers) {
         w.cap_bc = 1 << 22;
         KH_HIP(hipMalloc((void **)&w.bc, w.cap_bc * 8));
     }
+}
+
+// exclusive scan of n u32 counts into u64 offsets (rocPRIM decoupled look-back)
+static void scan_counts(Graph *g, const uint32_t *in, uint64_t *out, uint64_t n) {
+    Workspace &w = g->ws;
+    size_t bytes = 0;
+    KH_HIP(rocprim::exclusive_scan(nullptr, bytes, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(),
+                                   g->stream));
+    ensure(&w.scan_tmp, &w.cap_scan, bytes, 1);
+    bytes = w.cap_scan;
+    KH_HIP(rocprim::exclusive_scan(w.scan_tmp, bytes, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(),
+                                   g->stream));
 }
 
 void engine_sync_bigcounts(Graph *g) {
@@ -157,20 +202,27 @@ void engine_collect_events(Graph *g) {
 
 // LDS footprints
 static size_t lds_window(bool window, int tile_kmers) { return 16 + (window ? (size_t)(tile_kmers + 2) * 8 : 0); }
-static size_t lds_count_l1(const Params &P, bool window, int tile_kmers) {
-    return (size_t)((P.F1 + 3) & ~3u) * 4 + lds_window(window, tile_kmers);
+static size_t lds_hist_l1(const Params &P, bool window) {
+    return (size_t)((P.F1 + 3) & ~3u) * 4 + lds_window(window, L1_HIST_TILE);
 }
+// level-1 tail buffers (64 B per bucket) when they fit next to the tile
+static bool l1_tails(const Params &P) { return P.F1 <= 1024; }
 static size_t lds_scatter_l1(const Params &P, bool window, int tile_kmers) {
     const size_t F1a = (P.F1 + 3) & ~3u;
-    return F1a * 8 + (size_t)L1_TILE_RECS * 8 + F1a * 4 * 2 + (size_t)L1_TILE_RECS * 2 + lds_window(window, tile_kmers);
+    return F1a * 8 + (size_t)L1_TILE_RECS * 8 + (l1_tails(P) ? F1a * 64 : 0) + F1a * 4 * 2 +
+           (size_t)L1_TILE_RECS * 2 + ((F1a + 7) & ~7u) + lds_window(window, tile_kmers);
 }
 static size_t lds_scatter_l2(const Params &P) {
     const size_t F2 = (size_t)1 << P.s2;
-    return F2 * 8 + (size_t)L2_TILE_RECS * 8 + F2 * 4 * 2 + (size_t)L2_TILE_RECS * 2;
+    return F2 * 8 + (size_t)PT_TILE * 8 + F2 * 64 + F2 * 4 * 2 + F2;
+}
+static size_t lds_scatter_w(uint32_t FJ) {
+    const size_t FJa = (FJ + 3) & ~3u;
+    return FJa * 8 + (size_t)PT_TILE * 4 + FJa * 32 + FJa * 4 * 2 + FJa;
 }
 static size_t lds_apply(const Params &P) {
     const size_t R = (size_t)1 << P.s0;
-    return P.kind == BIT ? R * 4 + 16 + R / 8 : R * 4 * 2 + (R / 512) * 4 + R;
+    return P.kind == BIT ? R * 4 + 16 + 64 + R / 8 : R * 4 * 2 + (R / 512) * 4 + 64 + R / 8 + 16 + R;
 }
 
 // ---------------------------------------------------------------------------
@@ -178,13 +230,13 @@ static size_t lds_apply(const Params &P) {
 template <class Src>
 static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *out) {
     if (nkmers == 0) return;
-    if (nkmers > 0xFFFFFFF0ull) fail(KH_EVALUE, "batch too large");
-    ws_prepare(g, nkmers);
-    Workspace &w = g->ws;
+    if (nkmers > (1ull << 31)) fail(KH_EVALUE, "device batch too large (more than 2^31 k-mers)");
     const Params &P = g->prm;
+    const PassGeo q = pass_geo(P, nkmers);
+    ws_prepare(g, q);
+    Workspace &w = g->ws;
     hipStream_t st = g->stream;
     const uint64_t F1 = P.F1, F2 = 1ull << P.s2;
-    const uint64_t recs = nkmers * (uint64_t)P.n;
     const bool bigc = P.kind == BYTE && P.use_bigcount;
     const bool window = [&] {
         if constexpr (!Src::kReads) return false;
@@ -192,41 +244,42 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
     }();
     const uint64_t flag_bytes = (nkmers + 15) & ~15ull;
 
-    KH_HIP(hipMemsetAsync(w.cnt1, 0, F1 * 4, st));
-    KH_HIP(hipMemsetAsync(w.cnt2, 0, F1 * F2 * 4, st));
     KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
-    KH_HIP(hipMemsetAsync(w.newf, 0, flag_bytes, st));
     if (bigc) KH_HIP(hipMemsetAsync(w.fullf, 0, flag_bytes, st));
 
-    const int ctile = 4096;
-    const uint64_t nct = (nkmers + ctile - 1) / ctile;
-    TIMED("count_l1", hipLaunchKernelGGL(k_count_l1<Src>, dim3((unsigned)nct), dim3(L1_THREADS),
-                                         lds_count_l1(P, window, ctile), st, P, src, nkmers, ctile, w.cnt1));
-    TIMED("scan_l1", hipLaunchKernelGGL(k_scan_l1, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1,
-                                        w.cnt1, w.off1, w.cur1, w.tile1));
+    // level 1
+    TIMED("hist_l1", hipLaunchKernelGGL(k_hist_l1<Src>, dim3(q.nch1), dim3(L1_THREADS), lds_hist_l1(P, window), st, P,
+                                        src, nkmers, q.ck1, q.nch1, w.mcnt));
+    TIMED("scan", scan_counts(g, w.mcnt, w.moff, F1 * q.nch1));
+    TIMED("plan_l2", hipLaunchKernelGGL(k_plan_l2, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1, q.nch1,
+                                        w.moff, q.recs, w.off1, w.ch2));
     for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
         const int nt = std::min(L1_MAX_RPT, P.n - t0);
         const int kpt = std::max(1, L1_MAX_RPT / nt);
         const int tile_kmers = L1_THREADS * kpt;
-        const uint64_t ntiles = (nkmers + tile_kmers - 1) / tile_kmers;
-        TIMED("scatter_l1", hipLaunchKernelGGL(k_scatter_l1<Src>, dim3((unsigned)ntiles), dim3(L1_THREADS),
-                                               lds_scatter_l1(P, window, tile_kmers), st, P, src, nkmers, kpt, t0,
-                                               nt, w.cur1, w.rec1));
+        auto kfn = l1_tails(P) ? k_scatter_l1<Src, true> : k_scatter_l1<Src, false>;
+        TIMED("scatter_l1", hipLaunchKernelGGL(kfn, dim3(q.nch1), dim3(L1_THREADS), lds_scatter_l1(P, window, tile_kmers),
+                                               st, P, src, nkmers, q.ck1, q.nch1, kpt, t0, nt, w.moff, w.rec1));
     }
-    const uint64_t ntiles2 = (recs + L2_TILE_RECS - 1) / L2_TILE_RECS + F1;
-    TIMED("count_l2", hipLaunchKernelGGL(k_count_l2, dim3((unsigned)ntiles2), dim3(L2_THREADS), F2 * 4, st,
-                                         (uint32_t)F1, P.s0, P.s2, w.off1, w.tile1, w.rec1, w.cnt2));
-    TIMED("scan_l2", hipLaunchKernelGGL(k_scan_l2, dim3((unsigned)F1), dim3(1024), F2 * 8 + 1025 * 8, st, P.s2,
-                                        (uint32_t)F1, w.off1, w.cnt2, w.off2, w.cur2));
-    TIMED("scatter_l2", hipLaunchKernelGGL(k_scatter_l2, dim3((unsigned)ntiles2), dim3(L2_THREADS),
-                                           lds_scatter_l2(P), st, (uint32_t)F1, P.s0, P.s2, w.off1, w.tile1, w.cur2,
-                                           w.rec1, w.rec2));
+    // level 2
+    const unsigned g2 = (unsigned)q.nch2max;
+    TIMED("hist_l2", hipLaunchKernelGGL(k_hist_l2, dim3(g2), dim3(PT_THREADS), F2 * 4, st, (uint32_t)F1, P.s0, P.s2,
+                                        w.off1, w.ch2, w.rec1, w.mcnt));
+    TIMED("scan", scan_counts(g, w.mcnt, w.moff, F2 * q.nch2max));
+    TIMED("off2", hipLaunchKernelGGL(k_off2, dim3((unsigned)std::min<uint64_t>((F1 * F2 + 255) / 256, 8192)),
+                                     dim3(256), 0, st, (uint32_t)F1, P.s2, w.off1, w.ch2, w.moff, w.off2));
+    TIMED("scatter_l2", hipLaunchKernelGGL(k_scatter_l2, dim3(g2), dim3(PT_THREADS), lds_scatter_l2(P), st,
+                                           (uint32_t)F1, P.s0, P.s2, w.off1, w.ch2, w.moff, w.rec1, w.rec2));
 
+    // apply (winner segments -> first half of the dead level-1 buffer)
+    uint32_t *win = (uint32_t *)w.rec1;
+    uint32_t *wout = win + w.cap_recs;
     ApplyArgs A;
     A.off2 = w.off2;
     A.rec = w.rec2;
     A.tab = g->d_tab;
-    A.newf = w.newf;
+    A.win = win;
+    A.wcnt = w.wcnt;
     A.fullf = w.fullf;
     A.cross = w.cross;
     A.cap_cross = w.cap_cross;
@@ -234,8 +287,7 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
     A.rprefix[0] = 0;
     for (int i = 0; i < P.n; i++)
         A.rprefix[i + 1] = A.rprefix[i] + ((P.p[i] + (1ull << P.s0) - 1) >> P.s0);
-    const uint64_t real_regions = A.rprefix[P.n];
-    const unsigned agrid = (unsigned)std::min<uint64_t>(real_regions, 256 * 2 * 4);
+    const unsigned agrid = (unsigned)std::min<uint64_t>(q.regions, 256 * 2);
     if (P.kind == BIT)
         TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P), st, P, A));
     else if (P.kind == NIBBLE)
@@ -248,19 +300,38 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
         TIMED("crossing", hipLaunchKernelGGL(k_crossing, dim3(1024), dim3(256), 0, st, P, w.off2, w.rec2, w.cross,
                                              w.ctr, w.cap_cross, w.fullf));
 
+    // winners -> k-mer windows -> n_unique (+ per-k-mer new flags)
+    const bool want_new = out && out->h_new;
+    const size_t wmeta = W_RPC * 8 + (W_RPC + 4) * 4;
+    TIMED("hist_w", hipLaunchKernelGGL(k_hist_w, dim3(q.nchw), dim3(PT_THREADS), wmeta + (size_t)q.FJ * 4, st, P, A,
+                                       q.js, q.FJ, q.nchw, w.mcnt));
+    TIMED("scan", scan_counts(g, w.mcnt, w.moff, (uint64_t)q.FJ * q.nchw));
+    TIMED("scatter_w", hipLaunchKernelGGL(k_scatter_w, dim3(q.nchw), dim3(PT_THREADS), wmeta + lds_scatter_w(q.FJ), st,
+                                          P, A, q.js, q.FJ, q.nchw, w.moff, wout));
+    TIMED("mark", hipLaunchKernelGGL(k_mark, dim3(q.FJ), dim3(PT_THREADS), ((size_t)1 << q.js) / 8, st, wout, w.moff,
+                                     w.mcnt, q.nchw, q.FJ, q.js, w.ctr, want_new ? w.newbits : nullptr));
+
     uint64_t *d_out_hash = nullptr;
-    if (out && out->h_hash) d_out_hash = w.rec1;  // level-1 records are dead after scatter_l2
-    const uint64_t nchunk = flag_bytes / 16;
-    const unsigned fgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nchunk + FIN_THREADS - 1) / FIN_THREADS,
-                                                                              4096));
-    TIMED("finalize", hipLaunchKernelGGL(k_finalize<Src>, dim3(fgrid), dim3(FIN_THREADS), 0, st, P, src, nkmers,
-                                         w.newf, w.fullf, w.ctr, w.bc, w.cap_bc, d_out_hash));
+    if (out && out->h_hash) d_out_hash = w.rec2;  // level-2 records are dead after crossing
+    if (bigc || d_out_hash) {
+        const uint64_t nchunk = flag_bytes / 16;
+        const unsigned fgrid = (unsigned)std::max<uint64_t>(
+            1, std::min<uint64_t>((nchunk + FIN_THREADS - 1) / FIN_THREADS, 4096));
+        TIMED("finalize", hipLaunchKernelGGL(k_finalize<Src>, dim3(fgrid), dim3(FIN_THREADS), 0, st, P, src, nkmers,
+                                             w.fullf, w.ctr, w.bc, w.cap_bc, d_out_hash));
+    }
     KH_HIP(hipGetLastError());
     KH_HIP(hipMemcpyAsync(w.h_ctr, w.ctr, CTR_N * 8, hipMemcpyDeviceToHost, st));
-    if (out && out->h_new) KH_HIP(hipMemcpyAsync(out->h_new, w.newf, nkmers, hipMemcpyDeviceToHost, st));
+    std::vector<uint32_t> hbits;
+    if (want_new) {
+        hbits.resize((nkmers + 31) / 32);
+        KH_HIP(hipMemcpyAsync(hbits.data(), w.newbits, hbits.size() * 4, hipMemcpyDeviceToHost, st));
+    }
     if (d_out_hash) KH_HIP(hipMemcpyAsync(out->h_hash, d_out_hash, nkmers * 8, hipMemcpyDeviceToHost, st));
     KH_HIP(hipStreamSynchronize(st));
     engine_collect_events(g);
+    if (want_new)
+        for (uint64_t j = 0; j < nkmers; j++) out->h_new[j] = (uint8_t)((hbits[j >> 5] >> (j & 31)) & 1);
     if (w.h_ctr[CTR_ERR]) fail(KH_EDEVICE, "device overflow of crossing/bigcount buffers");
     g->n_occupied += w.h_ctr[CTR_OCC];
     g->n_unique += w.h_ctr[CTR_UNIQUE];
@@ -300,7 +371,7 @@ static void consume_reads(Graph *g, Src base, const uint64_t *d_koff, uint64_t n
     base.nreads = nreads;
     base.kbase = 0;
     base.rbase = 0;
-    if (out || nkmers <= B + (B >> 4)) {   // one pass (koff[0] == 0 by contract)
+    if (out || nkmers <= std::min<uint64_t>(B + (B >> 4), 1ull << 31)) {   // one pass (koff[0] == 0 by contract)
         run_pass(g, base, nkmers, out);
         return;
     }
@@ -517,11 +588,6 @@ void engine_synth_packed(int device, uint64_t seed, uint64_t r0, uint64_t nreads
 
 // ---------------------------------------------------------------------------
 // graph creation: table arena + partition geometry
-static int ceil_log2(uint64_t x) {
-    int s = 0;
-    while ((1ull << s) < x) s++;
-    return s;
-}
 
 void graph_prepare_params(Graph *g) {
     Params &P = g->prm;
@@ -564,6 +630,15 @@ static void set_lds_limits() {
     (void)hipFuncSetAttribute((const void *)k_apply_count<BYTE>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_bit, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcTwoBit, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcBytes, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcHashes, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcTwoBit, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcBytes, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcHashes, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_scatter_l2, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_scatter_w, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_mark, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipGetLastError();
 }
 
@@ -609,8 +684,8 @@ Graph::~Graph() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
     Workspace &w = ws;
-    void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.newf, w.fullf, w.bc, w.cnt1, w.off1,
-                    w.cur1, w.tile1, w.cnt2, w.off2, w.cur2, w.cross, w.ctr, w.d_words, w.d_koff, w.d_bytes,
+    void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.fullf, w.newbits, w.bc, w.off1, w.ch2,
+                    w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.cross, w.ctr, w.d_words, w.d_koff, w.d_bytes,
                     w.q_hashes, w.q_counts};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);

@@ -66,17 +66,18 @@ struct Params {
 struct Workspace {
     uint64_t cap_kmers = 0, cap_recs = 0;
     uint64_t *rec1 = nullptr, *rec2 = nullptr;   // (k-mer index << 32) | bin offset
-    uint8_t *newf = nullptr, *fullf = nullptr;   // per k-mer flags
+    uint8_t *fullf = nullptr;                    // per k-mer bigcount "full" tallies
+    uint32_t *newbits = nullptr;                 // per k-mer new flags (bitmap)
     uint64_t *bc = nullptr;                      // bigcount candidate hashes
-    uint64_t *hashes_out = nullptr;              // optional per-k-mer hashes
-    // bucket bookkeeping
-    uint32_t *cnt1 = nullptr;        // [F1]
-    uint64_t *off1 = nullptr;        // [F1+1]
-    uint64_t *cur1 = nullptr;        // [F1]
-    uint32_t *tile1 = nullptr;       // [F1+1] tile prefix of level-2 passes
-    uint32_t *cnt2 = nullptr;        // [F1*2^s2]
-    uint64_t *off2 = nullptr;        // [F1*2^s2 + 1]
-    uint64_t *cur2 = nullptr;        // [F1*2^s2]
+    // partition bookkeeping
+    uint64_t *off1 = nullptr;        // [F1+1] level-1 bucket offsets
+    uint32_t *ch2 = nullptr;         // [F1+1] level-2 chunk prefix per bucket
+    uint64_t *off2 = nullptr;        // [F1*2^s2 + 1] region offsets
+    uint32_t *mcnt = nullptr;        // (destination, chunk) count matrix
+    uint64_t *moff = nullptr;        // its exclusive scan
+    void *scan_tmp = nullptr;        // rocPRIM scan temporary storage
+    uint32_t *wcnt = nullptr;        // [regions] winners per region
+    uint64_t cap_m = 0, cap_moff = 0, cap_scan = 0, cap_newbits = 0, cap_wcnt = 0;
     uint64_t *cross = nullptr;       // crossing bins: (global bin << 8) | c0
     uint64_t *ctr = nullptr;         // counters, see CTR_*
     uint64_t *h_ctr = nullptr;       // pinned host mirror

@@ -1,14 +1,22 @@
-// kh_partition.cuh -- two-level partition of insert records (one record per
-// (k-mer, table)) into LDS-sized table regions.  Included by kh_engine.hip.
+// kh_partition.cuh -- partition of insert records (one per (k-mer, table))
+// into LDS-sized table regions, and of winner k-mer indices into k-mer
+// windows.  Included by kh_engine.hip.
 //
 // record = (batch k-mer index j << 32) | bin offset   (u64)
 //   level 1: offset inside a bucket of 2^(s0+s2) global bins
 //   level 2: offset inside a region of 2^s0 bins
-// Both scatters stage a tile in LDS sorted by destination (counting sort) and
-// write it out in contiguous runs (coalesced), one global cursor bump per
-// destination per tile.  Within a destination records are unordered; the
-// k-mer index travels with the record, so stream order is recovered exactly
-// in the apply step.
+//
+// Every partition is a chunked counting sort with NO returning global
+// atomics: a histogram kernel writes one count per (destination, chunk) into a
+// destination-major matrix, one device-wide exclusive scan (rocPRIM) turns it
+// into the exact output offset of every (destination, chunk) pair, and the
+// scatter kernel (one workgroup per chunk) keeps its cursors in LDS.  A chunk
+// is processed in tiles: each tile is counting-sorted in LDS and written out
+// in runs, and since a chunk's records for one destination are contiguous in
+// the output, consecutive tiles extend the same lines (write-combining in L2).
+// The result is deterministic and keeps the stream order of the k-mers at
+// tile granularity; exact stream order is recovered in the apply step from
+// the k-mer index carried by every record.
 #pragma once
 #include "kh_src.cuh"
 
@@ -16,10 +24,12 @@ namespace kh {
 
 constexpr int L1_THREADS = 512;
 constexpr int L1_MAX_RPT = 8;                      // records per thread per tile
-constexpr int L1_TILE_RECS = L1_THREADS * L1_MAX_RPT;
-constexpr int L2_THREADS = 1024;
-constexpr int L2_RPT = 8;
-constexpr int L2_TILE_RECS = L2_THREADS * L2_RPT;  // 8192
+constexpr int L1_TILE_RECS = L1_THREADS * L1_MAX_RPT;   // 4096
+constexpr int L1_HIST_TILE = 4096;                 // k-mers per histogram tile (window size)
+constexpr int PT_THREADS = 1024;                   // level-2 / winner partitions
+constexpr int PT_RPT = 8;
+constexpr int PT_TILE = PT_THREADS * PT_RPT;       // 8192
+constexpr uint64_t L2_CHUNK = 16ull * PT_TILE;     // records per level-2 chunk
 constexpr uint32_t NO_J = 0xFFFFFFFFu;
 
 // exclusive scan of hist[0..n) into lstart by one wave (n <= 8192)
@@ -39,30 +49,6 @@ __device__ __forceinline__ void wave_exclusive_scan(const uint32_t *hist, uint32
     for (uint32_t t = 0; t < per && b0 + t < n; t++) { lstart[b0 + t] = acc; acc += hist[b0 + t]; }
 }
 
-// ---------------------------------------------------------------------------
-// level 1: bucket histogram over all tables
-template <class Src>
-__global__ void __launch_bounds__(L1_THREADS) k_count_l1(Params P, Src src, uint64_t nkmers, int tile_kmers,
-                                                        uint32_t *cnt1) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t *hist = (uint32_t *)smem;
-    uint64_t *s_meta = (uint64_t *)(hist + ((P.F1 + 3) & ~3u));
-    uint64_t *s_koff = s_meta + 2;
-    const int shift = P.s0 + P.s2;
-    for (uint32_t b = threadIdx.x; b < P.F1; b += blockDim.x) hist[b] = 0;
-    const uint64_t j0 = (uint64_t)blockIdx.x * tile_kmers;
-    const uint64_t j1 = min(nkmers, j0 + tile_kmers);
-    TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
-    __syncthreads();
-    for (uint64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
-        const uint64_t h = kmer_hash(src, s_koff, tr, j);
-        for (int i = 0; i < P.n; i++) atomicAdd(&hist[global_bin(P, i, h) >> shift], 1u);
-    }
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < P.F1; b += blockDim.x)
-        if (hist[b]) atomicAdd(&cnt1[b], hist[b]);
-}
-
 // block-wide exclusive scan over n u64 values in LDS (blockDim.x == 1024)
 __device__ uint64_t block_exclusive_scan(uint64_t *v, uint32_t n, uint64_t *s_part) {
     const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
@@ -72,7 +58,6 @@ __device__ uint64_t block_exclusive_scan(uint64_t *v, uint32_t n, uint64_t *s_pa
     s_part[threadIdx.x] = sum;
     __syncthreads();
     if (threadIdx.x < 64) {
-        // 1024 partials scanned by one wave: 16 per lane
         const uint32_t lane = threadIdx.x;
         uint64_t loc = 0;
         for (int t = 0; t < 16; t++) loc += s_part[lane * 16 + t];
@@ -100,197 +85,283 @@ __device__ uint64_t block_exclusive_scan(uint64_t *v, uint32_t n, uint64_t *s_pa
     return s_part[1024];
 }
 
-// level-1 bucket offsets, their cursors, and the tile prefix of level 2
-__global__ void __launch_bounds__(1024) k_scan_l1(uint32_t F1, const uint32_t *cnt1, uint64_t *off1,
-                                                  uint64_t *cur1, uint32_t *tile1) {
+// ---------------------------------------------------------------------------
+// Tail-buffered emission of a counting-sorted LDS tile.  Destination d's
+// records of the tile go to out[lcur[d] ...]; only whole aligned segments of
+// SEG records are written, the remainder waits in an LDS tail slot until its
+// segment completes or the chunk ends.  Every write is then a full 64-B (or
+// 32-B) segment except the first one of each (chunk, destination) run, which
+// it shares with the previous chunk.  TAILS == false writes runs directly.
+template <class T, int SEG, bool TAILS>
+struct Emit {
+    uint64_t *lcur;    // [F] next output position
+    uint8_t *hskip;    // [F] slots of the head segment owned by the previous chunk
+    T *tail;           // [F*SEG]
+    uint32_t *hist;    // [F] this tile's count
+    uint32_t *lstart;  // [F] this tile's LDS start
+
+    __device__ __forceinline__ void init(uint32_t d, uint64_t pos) const {
+        lcur[d] = pos;
+        if (TAILS) hskip[d] = (uint8_t)(pos & (SEG - 1));
+        hist[d] = 0;
+    }
+    __device__ __forceinline__ uint64_t flush_end(uint64_t e, bool last) const {
+        return last ? e : (e & ~(uint64_t)(SEG - 1));
+    }
+    // phase 1 (after the tile is staged): write tails whose segment completes
+    __device__ __forceinline__ void flush_tails(uint32_t F, bool last, T *out) const {
+        if (!TAILS) return;
+        for (uint32_t x = threadIdx.x; x < F * SEG; x += blockDim.x) {
+            const uint32_t d = x / SEG, sl = x % SEG;
+            const uint64_t lc = lcur[d];
+            const uint64_t a = lc & ~(uint64_t)(SEG - 1);
+            if (lc == a || flush_end(lc + hist[d], last) <= a) continue;
+            if (sl >= hskip[d] && a + sl < lc) out[a + sl] = tail[x];
+        }
+    }
+    // phase 2 (after a barrier): staged record q of destination d
+    __device__ __forceinline__ void put(uint32_t d, uint32_t q, T v, bool last, T *out) const {
+        const uint64_t pos = lcur[d] + (q - lstart[d]);
+        if (!TAILS || pos < flush_end(lcur[d] + hist[d], last)) out[pos] = v;
+        else tail[d * SEG + (uint32_t)(pos & (SEG - 1))] = v;
+    }
+    // phase 3 (after a barrier): advance cursors, clear the tile histogram
+    __device__ __forceinline__ void advance(uint32_t F, bool last) const {
+        for (uint32_t d = threadIdx.x; d < F; d += blockDim.x) {
+            const uint64_t lc = lcur[d], e = lc + hist[d];
+            if (TAILS && flush_end(e, last) > (lc & ~(uint64_t)(SEG - 1))) hskip[d] = 0;
+            lcur[d] = e;
+            hist[d] = 0;
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------
+// level 1: per-chunk bucket histogram over all tables -> M1[b * nch1 + chunk]
+template <class Src>
+__global__ void __launch_bounds__(L1_THREADS) k_hist_l1(Params P, Src src, uint64_t nkmers, uint32_t ck1,
+                                                       uint32_t nch1, uint32_t *M1) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *hist = (uint32_t *)smem;
+    uint64_t *s_meta = (uint64_t *)(hist + ((P.F1 + 3) & ~3u));
+    uint64_t *s_koff = s_meta + 2;
+    const int shift = P.s0 + P.s2;
+    for (uint32_t b = threadIdx.x; b < P.F1; b += blockDim.x) hist[b] = 0;
+    const uint64_t c0 = (uint64_t)blockIdx.x * ck1;
+    const uint64_t c1 = min(nkmers, c0 + ck1);
+    for (uint64_t j0 = c0; j0 < c1; j0 += L1_HIST_TILE) {
+        const uint64_t j1 = min(c1, j0 + L1_HIST_TILE);
+        __syncthreads();
+        TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
+        for (uint64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
+            const uint64_t h = kmer_hash(src, s_koff, tr, j);
+            for (int i = 0; i < P.n; i++) atomicAdd(&hist[global_bin(P, i, h) >> shift], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < P.F1; b += blockDim.x) M1[(uint64_t)b * nch1 + blockIdx.x] = hist[b];
+}
+
+// level-1 bucket offsets (from the scanned matrix) and the level-2 chunk
+// prefix: bucket b owns level-2 chunks [ch2[b], ch2[b+1])
+__global__ void __launch_bounds__(1024) k_plan_l2(uint32_t F1, uint32_t nch1, const uint64_t *O1, uint64_t total,
+                                                  uint64_t *off1, uint32_t *ch2) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t *v = (uint64_t *)smem;   // [F1]
     uint64_t *s_part = v + F1;        // [1025]
-    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) v[b] = cnt1[b];
-    __syncthreads();
-    const uint64_t total = block_exclusive_scan(v, F1, s_part);
-    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) { off1[b] = v[b]; cur1[b] = v[b]; }
+    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) {
+        const uint64_t s = O1[(uint64_t)b * nch1];
+        const uint64_t e = b + 1 < F1 ? O1[(uint64_t)(b + 1) * nch1] : total;
+        off1[b] = s;
+        v[b] = (e - s + L2_CHUNK - 1) / L2_CHUNK;
+    }
     if (threadIdx.x == 0) off1[F1] = total;
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) v[b] = (cnt1[b] + L2_TILE_RECS - 1) / L2_TILE_RECS;
-    __syncthreads();
-    const uint64_t tiles = block_exclusive_scan(v, F1, s_part);
-    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) tile1[b] = (uint32_t)v[b];
-    if (threadIdx.x == 0) tile1[F1] = (uint32_t)tiles;
+    const uint64_t chunks = block_exclusive_scan(v, F1, s_part);
+    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) ch2[b] = (uint32_t)v[b];
+    if (threadIdx.x == 0) ch2[F1] = (uint32_t)chunks;
 }
 
-// level-1 scatter of tables [t0, t0+nt) (nt <= 8): records are kept in
-// registers between the histogram and the placement pass
-template <class Src>
-__global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, uint64_t nkmers, int kpt, int t0,
-                                                          int nt, uint64_t *cur1, uint64_t *rec) {
+// level-1 scatter of tables [t0, t0+nt) (nt <= 8), one workgroup per chunk;
+// records stay in registers between the tile histogram and the placement.
+// The chunk's cursors are written back so a following table group continues.
+template <class Src, bool TAILS>
+__global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, uint64_t nkmers, uint32_t ck1,
+                                                          uint32_t nch1, int kpt, int t0, int nt, uint64_t *O1,
+                                                          uint64_t *rec) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t F1 = P.F1;
     const uint32_t F1a = (F1 + 3) & ~3u;
-    uint64_t *gbase = (uint64_t *)smem;               // [F1]
-    uint64_t *stage = gbase + F1a;                    // [L1_TILE_RECS]
-    uint32_t *hist = (uint32_t *)(stage + L1_TILE_RECS);  // [F1]
+    uint64_t *lcur = (uint64_t *)smem;                // [F1]
+    uint64_t *stage = lcur + F1a;                     // [L1_TILE_RECS]
+    uint64_t *tail = stage + L1_TILE_RECS;            // [F1*8] (TAILS)
+    uint32_t *hist = (uint32_t *)(tail + (TAILS ? F1a * 8 : 0));  // [F1]
     uint32_t *lstart = hist + F1a;                    // [F1]
     uint16_t *sb = (uint16_t *)(lstart + F1a);        // [L1_TILE_RECS]
-    uint64_t *s_meta = (uint64_t *)(sb + L1_TILE_RECS);
+    uint8_t *hskip = (uint8_t *)(sb + L1_TILE_RECS);  // [F1]
+    uint64_t *s_meta = (uint64_t *)(hskip + ((F1a + 7) & ~7u));
     uint64_t *s_koff = s_meta + 2;
+    const Emit<uint64_t, 8, TAILS> em{lcur, hskip, tail, hist, lstart};
     const int shift = P.s0 + P.s2;
     const uint64_t omask = (1ull << shift) - 1;
     const int tile_kmers = L1_THREADS * kpt;
 
-    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) hist[b] = 0;
-    const uint64_t j0 = (uint64_t)blockIdx.x * tile_kmers;
-    const uint64_t j1 = min(nkmers, j0 + tile_kmers);
-    TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
-    __syncthreads();
-
-    uint64_t G[L1_MAX_RPT];
-    uint32_t rank[L1_MAX_RPT];
-    uint32_t jj[L1_MAX_RPT];
-    int nr = 0;
+    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) em.init(b, O1[(uint64_t)b * nch1 + blockIdx.x]);
+    const uint64_t c0 = (uint64_t)blockIdx.x * ck1;
+    const uint64_t c1 = min(nkmers, c0 + ck1);
+    for (uint64_t j0 = c0; j0 < c1; j0 += tile_kmers) {
+        const uint64_t j1 = min(c1, j0 + tile_kmers);
+        const bool last = j1 == c1;
+        __syncthreads();
+        TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
+        uint64_t G[L1_MAX_RPT];
+        uint32_t rank[L1_MAX_RPT];
+        uint32_t jj[L1_MAX_RPT];
+        int nr = 0;
 #pragma unroll
-    for (int q = 0; q < L1_MAX_RPT; q++) { G[q] = 0; rank[q] = 0; jj[q] = 0; }
-    // pass A: hash, bins, bucket histogram (ranks within the tile)
-    for (int a = 0; a < kpt; a++) {
-        const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
-        if (j >= j1) break;
-        const uint64_t h = kmer_hash(src, s_koff, tr, j);
+        for (int q = 0; q < L1_MAX_RPT; q++) { G[q] = 0; rank[q] = 0; jj[q] = 0; }
+        // pass A: hash, bins, tile histogram (ranks)
+        for (int a = 0; a < kpt; a++) {
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            if (j >= j1) break;
+            const uint64_t h = kmer_hash(src, s_koff, tr, j);
 #pragma unroll
-        for (int q = 0; q < L1_MAX_RPT; q++) {
-            const int i = q - a * nt;  // table slot of register q for k-mer a
-            if (i >= 0 && i < nt) {
-                G[q] = global_bin(P, t0 + i, h);
-                jj[q] = (uint32_t)j;
-                rank[q] = atomicAdd(&hist[(uint32_t)(G[q] >> shift)], 1u);
-                nr = q + 1;
+            for (int q = 0; q < L1_MAX_RPT; q++) {
+                const int i = q - a * nt;  // table slot of register q for k-mer a
+                if (i >= 0 && i < nt) {
+                    G[q] = global_bin(P, t0 + i, h);
+                    jj[q] = (uint32_t)j;
+                    rank[q] = atomicAdd(&hist[(uint32_t)(G[q] >> shift)], 1u);
+                    nr = q + 1;
+                }
             }
         }
-    }
-    __syncthreads();
-    wave_exclusive_scan(hist, lstart, F1);
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x)
-        if (hist[b]) gbase[b] = atomicAdd((unsigned long long *)&cur1[b], (unsigned long long)hist[b]);
-    // pass B: place in LDS in bucket order
+        __syncthreads();
+        wave_exclusive_scan(hist, lstart, F1);
+        __syncthreads();
+        // pass B: place in LDS in bucket order
 #pragma unroll
-    for (int q = 0; q < L1_MAX_RPT; q++) {
-        if (q < nr) {
-            const uint32_t b = (uint32_t)(G[q] >> shift);
-            const uint32_t pos = lstart[b] + rank[q];
-            stage[pos] = ((uint64_t)jj[q] << 32) | (G[q] & omask);
-            sb[pos] = (uint16_t)b;
+        for (int q = 0; q < L1_MAX_RPT; q++) {
+            if (q < nr) {
+                const uint32_t b = (uint32_t)(G[q] >> shift);
+                const uint32_t pos = lstart[b] + rank[q];
+                stage[pos] = ((uint64_t)jj[q] << 32) | (G[q] & omask);
+                sb[pos] = (uint16_t)b;
+            }
         }
+        em.flush_tails(F1, last, rec);
+        __syncthreads();
+        // pass C: whole segments at the chunk's cursors
+        const uint32_t nrec = (uint32_t)((j1 - j0) * (uint64_t)nt);
+        for (uint32_t q = threadIdx.x; q < nrec; q += blockDim.x) em.put(sb[q], q, stage[q], last, rec);
+        __syncthreads();
+        em.advance(F1, last);
     }
     __syncthreads();
-    // pass C: coalesced runs
-    const uint32_t nrec = (P.ablate & 8) ? 0 : (uint32_t)((j1 - j0) * (uint64_t)nt);
-    for (uint32_t q = threadIdx.x; q < nrec; q += blockDim.x) {
-        const uint32_t b = sb[q];
-        rec[gbase[b] + (q - lstart[b])] = stage[q];
-    }
+    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) O1[(uint64_t)b * nch1 + blockIdx.x] = lcur[b];
 }
 
 // ---------------------------------------------------------------------------
-// level 2
-__device__ __forceinline__ bool l2_tile(uint32_t F1, const uint64_t *off1, const uint32_t *tile1,
-                                        uint32_t *bucket, uint64_t *r0, uint64_t *r1) {
+// level 2: chunk t of the level-1 output lies in bucket b (ch2[b] <= t < ch2[b+1])
+struct L2Chunk {
+    uint32_t b, c, nc;
+    uint64_t r0, r1;
+};
+
+__device__ __forceinline__ bool l2_chunk(uint32_t F1, const uint64_t *off1, const uint32_t *ch2, L2Chunk *k) {
     const uint32_t t = blockIdx.x;
-    if (t >= tile1[F1]) return false;
-    uint32_t lo = 0, hi = F1;  // tile1[lo] <= t < tile1[hi]
+    if (t >= ch2[F1]) return false;
+    uint32_t lo = 0, hi = F1;  // largest lo with ch2[lo] <= t (a non-empty bucket)
     while (hi - lo > 1) {
         uint32_t mid = (lo + hi) >> 1;
-        if (tile1[mid] <= t) lo = mid; else hi = mid;
+        if (ch2[mid] <= t) lo = mid; else hi = mid;
     }
-    *bucket = lo;
-    const uint64_t s = off1[lo] + (uint64_t)(t - tile1[lo]) * L2_TILE_RECS;
-    *r0 = s;
-    *r1 = min(off1[lo + 1], s + L2_TILE_RECS);
+    k->b = lo;
+    k->c = t - ch2[lo];
+    k->nc = ch2[lo + 1] - ch2[lo];
+    k->r0 = off1[lo] + (uint64_t)k->c * L2_CHUNK;
+    k->r1 = min(off1[lo + 1], k->r0 + L2_CHUNK);
     return true;
 }
 
-__global__ void __launch_bounds__(L2_THREADS) k_count_l2(uint32_t F1, int s0, int s2, const uint64_t *off1,
-                                                        const uint32_t *tile1, const uint64_t *rec,
-                                                        uint32_t *cnt2) {
+// matrix layout: bucket b, region r, chunk c -> ch2[b]*F2 + r*nc + c; one
+// exclusive scan over it gives absolute level-2 offsets (bucket b starts at
+// off1[b] automatically)
+__global__ void __launch_bounds__(PT_THREADS) k_hist_l2(uint32_t F1, int s0, int s2, const uint64_t *off1,
+                                                       const uint32_t *ch2, const uint64_t *rec, uint32_t *M2) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *hist = (uint32_t *)smem;
     const uint32_t F2 = 1u << s2;
-    uint32_t b;
-    uint64_t r0, r1;
-    if (!l2_tile(F1, off1, tile1, &b, &r0, &r1)) return;
+    L2Chunk k;
+    if (!l2_chunk(F1, off1, ch2, &k)) return;
     for (uint32_t r = threadIdx.x; r < F2; r += blockDim.x) hist[r] = 0;
     __syncthreads();
     const uint32_t *rec32 = (const uint32_t *)rec;   // low words = offsets
-    for (uint64_t q = r0 + threadIdx.x; q < r1; q += blockDim.x) atomicAdd(&hist[rec32[2 * q] >> s0], 1u);
+    for (uint64_t q = k.r0 + threadIdx.x; q < k.r1; q += blockDim.x) atomicAdd(&hist[rec32[2 * q] >> s0], 1u);
     __syncthreads();
-    for (uint32_t r = threadIdx.x; r < F2; r += blockDim.x)
-        if (hist[r]) atomicAdd(&cnt2[(uint64_t)b * F2 + r], hist[r]);
+    const uint64_t base = (uint64_t)ch2[k.b] * F2 + k.c;
+    for (uint32_t r = threadIdx.x; r < F2; r += blockDim.x) M2[base + (uint64_t)r * k.nc] = hist[r];
 }
 
-// per bucket: absolute region offsets in the level-2 record array
-__global__ void __launch_bounds__(1024) k_scan_l2(int s2, uint32_t F1, const uint64_t *off1, const uint32_t *cnt2,
-                                                  uint64_t *off2, uint64_t *cur2) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// region offsets for the apply step
+__global__ void k_off2(uint32_t F1, int s2, const uint64_t *off1, const uint32_t *ch2, const uint64_t *O2,
+                       uint64_t *off2) {
     const uint32_t F2 = 1u << s2;
-    uint64_t *v = (uint64_t *)smem;   // [F2]
-    uint64_t *s_part = v + F2;        // [1025]
-    const uint32_t b = blockIdx.x;
-    for (uint32_t r = threadIdx.x; r < F2; r += blockDim.x) v[r] = cnt2[(uint64_t)b * F2 + r];
-    __syncthreads();
-    block_exclusive_scan(v, F2, s_part);
-    const uint64_t base = off1[b];
-    for (uint32_t r = threadIdx.x; r < F2; r += blockDim.x) {
-        off2[(uint64_t)b * F2 + r] = base + v[r];
-        cur2[(uint64_t)b * F2 + r] = base + v[r];
+    const uint64_t nreg = (uint64_t)F1 * F2;
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < nreg; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t b = (uint32_t)(g >> s2), r = (uint32_t)(g & (F2 - 1));
+        const uint32_t nc = ch2[b + 1] - ch2[b];
+        off2[g] = nc ? O2[(uint64_t)ch2[b] * F2 + (uint64_t)r * nc] : off1[b];
     }
-    if (b == F1 - 1 && threadIdx.x == 0) off2[(uint64_t)F1 * F2] = off1[F1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) off2[nreg] = off1[F1];
 }
 
-__global__ void __launch_bounds__(L2_THREADS) k_scatter_l2(uint32_t F1, int s0, int s2, const uint64_t *off1,
-                                                          const uint32_t *tile1, uint64_t *cur2,
+__global__ void __launch_bounds__(PT_THREADS) k_scatter_l2(uint32_t F1, int s0, int s2, const uint64_t *off1,
+                                                          const uint32_t *ch2, const uint64_t *O2,
                                                           const uint64_t *rec_in, uint64_t *rec_out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t F2 = 1u << s2;
-    uint64_t *gbase = (uint64_t *)smem;            // [F2]
-    uint64_t *stage = gbase + F2;                  // [L2_TILE_RECS]
-    uint32_t *hist = (uint32_t *)(stage + L2_TILE_RECS);  // [F2]
+    uint64_t *lcur = (uint64_t *)smem;             // [F2]
+    uint64_t *stage = lcur + F2;                   // [PT_TILE] level-1 records
+    uint64_t *tail = stage + PT_TILE;              // [F2*8]
+    uint32_t *hist = (uint32_t *)(tail + F2 * 8);  // [F2]
     uint32_t *lstart = hist + F2;                  // [F2]
-    uint16_t *sr = (uint16_t *)(lstart + F2);      // [L2_TILE_RECS]
+    uint8_t *hskip = (uint8_t *)(lstart + F2);     // [F2]
+    const Emit<uint64_t, 8, true> em{lcur, hskip, tail, hist, lstart};
     const uint64_t rmask = (1ull << s0) - 1;
-    uint32_t b;
-    uint64_t r0, r1;
-    if (!l2_tile(F1, off1, tile1, &b, &r0, &r1)) return;
-    for (uint32_t r = threadIdx.x; r < F2; r += blockDim.x) hist[r] = 0;
-    __syncthreads();
-    uint64_t v[L2_RPT];
-    uint32_t rank[L2_RPT];
+    L2Chunk k;
+    if (!l2_chunk(F1, off1, ch2, &k)) return;
+    const uint64_t base = (uint64_t)ch2[k.b] * F2 + k.c;
+    for (uint32_t r = threadIdx.x; r < F2; r += blockDim.x) em.init(r, O2[base + (uint64_t)r * k.nc]);
+    for (uint64_t t0 = k.r0; t0 < k.r1; t0 += PT_TILE) {
+        const uint64_t t1 = min(k.r1, t0 + PT_TILE);
+        const bool last = t1 == k.r1;
+        __syncthreads();
+        uint64_t v[PT_RPT];
+        uint32_t rank[PT_RPT];
 #pragma unroll
-    for (int q = 0; q < L2_RPT; q++) {
-        const uint64_t idx = r0 + (uint64_t)q * L2_THREADS + threadIdx.x;
-        v[q] = idx < r1 ? rec_in[idx] : ~0ull;
-    }
-#pragma unroll
-    for (int q = 0; q < L2_RPT; q++)
-        if (v[q] != ~0ull) rank[q] = atomicAdd(&hist[(uint32_t)v[q] >> s0], 1u);
-    __syncthreads();
-    wave_exclusive_scan(hist, lstart, F2);
-    __syncthreads();
-    for (uint32_t r = threadIdx.x; r < F2; r += blockDim.x)
-        if (hist[r]) gbase[r] = atomicAdd((unsigned long long *)&cur2[(uint64_t)b * F2 + r],
-                                          (unsigned long long)hist[r]);
-#pragma unroll
-    for (int q = 0; q < L2_RPT; q++) {
-        if (v[q] != ~0ull) {
-            const uint32_t r = (uint32_t)v[q] >> s0;
-            const uint32_t pos = lstart[r] + rank[q];
-            stage[pos] = (v[q] & ~0xFFFFFFFFull) | (v[q] & rmask);
-            sr[pos] = (uint16_t)r;
+        for (int q = 0; q < PT_RPT; q++) {
+            const uint64_t idx = t0 + (uint64_t)q * PT_THREADS + threadIdx.x;
+            v[q] = idx < t1 ? rec_in[idx] : ~0ull;
         }
-    }
-    __syncthreads();
-    const uint32_t nrec = (uint32_t)(r1 - r0);
-    for (uint32_t q = threadIdx.x; q < nrec; q += blockDim.x) {
-        const uint32_t r = sr[q];
-        rec_out[gbase[r] + (q - lstart[r])] = stage[q];
+#pragma unroll
+        for (int q = 0; q < PT_RPT; q++)
+            if (v[q] != ~0ull) rank[q] = atomicAdd(&hist[(uint32_t)v[q] >> s0], 1u);
+        __syncthreads();
+        wave_exclusive_scan(hist, lstart, F2);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PT_RPT; q++)
+            if (v[q] != ~0ull) stage[lstart[(uint32_t)v[q] >> s0] + rank[q]] = v[q];
+        em.flush_tails(F2, last, rec_out);
+        __syncthreads();
+        const uint32_t nrec = (uint32_t)(t1 - t0);
+        for (uint32_t q = threadIdx.x; q < nrec; q += blockDim.x) {
+            const uint64_t x = stage[q];
+            em.put((uint32_t)x >> s0, q, (x & ~0xFFFFFFFFull) | (x & rmask), last, rec_out);
+        }
+        __syncthreads();
+        em.advance(F2, last);
     }
 }
 
