@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
             for (uint32_t x = t; x < R / 32; x += blockDim.x) full255[x] = 0;
             if (t == 0) s_flag[0] = 0;
         }
-        __syncthreads();
+        block_sync();
         // records: the prefetched batch, then APPLY_RECS loads in flight per thread
         if (!(P.ablate & 2)) {
 #pragma unroll
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
                 for (int u = 0; u < APPLY_RECS; u++) count_record(v[u], cnt, minj);
             }
         }
-        __syncthreads();
+        block_sync();
         prefetch_region<KIND>(P, A, rr + gridDim.x, total, nxt);
         // pass 1 (thread per bin, conflict-free LDS): winners (bins zero
         // before the batch keep their minimum k-mer index, the others drop
@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
         }
         if (P.ablate & 1) nw = 0;
         const uint32_t wex = wave_winner_scan(nw, s_wt);
-        __syncthreads();
+        block_sync();
         // pass 2: write back changed 16-bin chunks; winners to the region's segment
         for (uint32_t x = t; x < nchunk; x += blockDim.x) {
             if (!((chg[x >> 5] >> (x & 31)) & 1) || (P.ablate & 4)) continue;
@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
             }
         }
         if (t == 0) A.wcnt[rr] = wall;
-        __syncthreads();
+        block_sync();
         cur = nxt;
     }
     occ = wave_sum(occ);
@@ -325,7 +325,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyA
         if (t < nchunk) ((uint4 *)bits)[t] = cur.tv;
         for (uint32_t x = t; x < nchunk * 32; x += blockDim.x) ((uint4 *)minj)[x] = make_uint4(NO_J, NO_J, NO_J, NO_J);
         if (t < 4) chg[t] = 0;
-        __syncthreads();
+        block_sync();
 #pragma unroll
         for (int u = 0; u < APPLY_RECS; u++) bit_record(cur.v[u], minj);
         const uint64_t step = (uint64_t)APPLY_RECS * APPLY_THREADS;
@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyA
 #pragma unroll
             for (int u = 0; u < APPLY_RECS; u++) bit_record(v[u], minj);
         }
-        __syncthreads();
+        block_sync();
         prefetch_region<BIT>(P, A, rr + gridDim.x, total, nxt);
         // pass 1 (thread per bin): winners set their bit
         uint32_t nw = 0;
@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyA
             occ += (ri.i == 0);
         }
         const uint32_t wex = wave_winner_scan(nw, s_wt);
-        __syncthreads();
+        block_sync();
         // pass 2: write back changed 128-bin chunks; winners
         for (uint32_t x = t; x < nchunk; x += blockDim.x)
             if ((chg[x >> 5] >> (x & 31)) & 1) ((uint4 *)tab)[x] = ((const uint4 *)bits)[x];
@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyA
             }
         }
         if (t == 0) A.wcnt[rr] = wall;
-        __syncthreads();
+        block_sync();
         cur = nxt;
     }
     occ = wave_sum(occ);
@@ -397,7 +397,7 @@ __device__ __forceinline__ uint32_t w_chunk_setup(const Params &P, const ApplyAr
         s_pre[lane + 1] = incl;
         if (lane == 0) s_pre[0] = 0;
     }
-    __syncthreads();
+    block_sync();
     return s_pre[W_RPC];
 }
 __device__ __forceinline__ uint32_t w_elem(const ApplyArgs &A, const uint32_t *s_pre, const uint64_t *s_e0,
@@ -419,49 +419,58 @@ __global__ void __launch_bounds__(PT_THREADS) k_hist_w(Params P, ApplyArgs A, in
     for (uint32_t b = threadIdx.x; b < FJ; b += blockDim.x) hist[b] = 0;
     const uint32_t n = w_chunk_setup(P, A, A.rprefix[P.n], s_pre, s_e0);
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[w_elem(A, s_pre, s_e0, i) >> js], 1u);
-    __syncthreads();
+    block_sync();
     for (uint32_t b = threadIdx.x; b < FJ; b += blockDim.x) M3[(uint64_t)b * nchw + blockIdx.x] = hist[b];
 }
 
-__global__ void __launch_bounds__(PT_THREADS) k_scatter_w(Params P, ApplyArgs A, int js, uint32_t FJ, uint32_t nchw,
-                                                         const uint64_t *O3, uint32_t *wout) {
+template <int THREADS, int SEG>
+__global__ void __launch_bounds__(THREADS) k_scatter_w(Params P, ApplyArgs A, int js, uint32_t FJ, uint32_t nchw,
+                                                      const uint64_t *O3, uint32_t *wout) {
+    constexpr int TILE = THREADS * PT_RPT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t FJa = (FJ + 3) & ~3u;
     uint64_t *s_e0 = (uint64_t *)smem;             // [W_RPC]
     uint32_t *s_pre = (uint32_t *)(s_e0 + W_RPC);  // [W_RPC + 1]
     uint64_t *lcur = (uint64_t *)(s_pre + W_RPC + 4);  // [FJ]  (W_RPC + 4 keeps 8-B alignment)
-    uint32_t *stage = (uint32_t *)(lcur + FJa);    // [PT_TILE]
-    uint32_t *tail = stage + PT_TILE;              // [FJ*8]
-    uint32_t *hist = tail + FJa * 8;               // [FJ]
+    uint32_t *stage = (uint32_t *)(lcur + FJa);    // [TILE]
+    uint32_t *tail = stage + TILE;                 // [FJ*SEG]
+    uint32_t *hist = tail + (SEG > 1 ? FJa * SEG : 0); // [FJ]
     uint32_t *lstart = hist + FJa;                 // [FJ]
-    uint8_t *hskip = (uint8_t *)(lstart + FJa);    // [FJ]
-    const Emit<uint32_t, 8, true> em{lcur, hskip, tail, hist, lstart};
-    for (uint32_t b = threadIdx.x; b < FJ; b += blockDim.x) em.init(b, O3[(uint64_t)b * nchw + blockIdx.x]);
+    uint32_t *s_wtot = lstart + FJa;               // [16]
+    uint8_t *hskip = (uint8_t *)(s_wtot + 16);     // [FJ]
+    const Emit<uint32_t, SEG> em{lcur, hskip, tail, hist, lstart};
+    for (uint32_t b = threadIdx.x; b < FJ; b += THREADS) em.init(b, O3[(uint64_t)b * nchw + blockIdx.x]);
     const uint32_t n = w_chunk_setup(P, A, A.rprefix[P.n], s_pre, s_e0);
-    for (uint32_t t0 = 0; t0 < n; t0 += PT_TILE) {
-        const uint32_t t1 = min(n, t0 + PT_TILE);
-        const bool last = t1 == n;
-        __syncthreads();
+    const uint32_t ntiles = uniform_u32((n + TILE - 1) / TILE);
+    for (uint32_t ti = 0; ti < ntiles; ti++) {
+        const uint32_t t0 = ti * TILE;
+        const uint32_t t1 = min(n, t0 + TILE);
+        const bool last = ti + 1 == ntiles;
+        block_sync();
         uint32_t v[PT_RPT], rank[PT_RPT];
 #pragma unroll
         for (int q = 0; q < PT_RPT; q++) {
-            const uint32_t idx = t0 + (uint32_t)q * PT_THREADS + threadIdx.x;
+            const uint32_t idx = t0 + (uint32_t)q * THREADS + threadIdx.x;
             v[q] = idx < t1 ? w_elem(A, s_pre, s_e0, idx) : NO_J;
         }
 #pragma unroll
         for (int q = 0; q < PT_RPT; q++)
             if (v[q] != NO_J) rank[q] = atomicAdd(&hist[v[q] >> js], 1u);
-        __syncthreads();
-        wave_exclusive_scan(hist, lstart, FJ);
-        __syncthreads();
+        block_sync();
+        block_scan_hist(hist, lstart, FJ, s_wtot);
+        block_sync();
 #pragma unroll
         for (int q = 0; q < PT_RPT; q++)
             if (v[q] != NO_J) stage[lstart[v[q] >> js] + rank[q]] = v[q];
         em.flush_tails(FJ, last, wout);
-        __syncthreads();
+        block_sync();
         const uint32_t nrec = t1 - t0;
-        for (uint32_t q = threadIdx.x; q < nrec; q += blockDim.x) em.put(stage[q] >> js, q, stage[q], last, wout);
-        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PT_RPT; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * THREADS;
+            if (q < nrec) em.put(stage[q] >> js, q, stage[q], last, wout);
+        }
+        block_sync();
         em.advance(FJ, last);
     }
 }
@@ -479,13 +488,13 @@ __global__ void __launch_bounds__(PT_THREADS) k_mark(const uint32_t *wout, const
     const uint64_t last = (uint64_t)FJ * nchw - 1;
     const uint64_t e = jb + 1 < FJ ? O3[(uint64_t)(jb + 1) * nchw] : O3[last] + M3[last];
     for (uint32_t t = threadIdx.x; t < nw / 4; t += blockDim.x) ((uint4 *)bits)[t] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
+    block_sync();
     const uint32_t mask = (1u << js) - 1;
     for (uint64_t q = s + threadIdx.x; q < e; q += blockDim.x) {
         const uint32_t j = wout[q] & mask;
         atomicOr(&bits[j >> 5], 1u << (j & 31));
     }
-    __syncthreads();
+    block_sync();
     uint64_t uniq = 0;
     for (uint32_t t = threadIdx.x; t < nw / 4; t += blockDim.x) {
         const uint4 x = ((const uint4 *)bits)[t];
@@ -519,7 +528,7 @@ __global__ void __launch_bounds__(256) k_crossing(Params P, const uint64_t *off2
         for (int pass = 0; pass < 4; pass++) {
             const int sh = 24 - 8 * pass;
             for (int t = threadIdx.x; t < 256; t += blockDim.x) hist[t] = 0;
-            __syncthreads();
+            block_sync();
             for (uint64_t q = e0 + threadIdx.x; q < e1; q += blockDim.x) {
                 const uint64_t v = rec[q];
                 if ((uint32_t)v != o) continue;
@@ -527,7 +536,7 @@ __global__ void __launch_bounds__(256) k_crossing(Params P, const uint64_t *off2
                 if (pass > 0 && (j >> (sh + 8)) != (prefix >> (sh + 8))) continue;
                 atomicAdd(&hist[(j >> sh) & 0xFF], 1u);
             }
-            __syncthreads();
+            block_sync();
             if (threadIdx.x == 0) {
                 uint32_t acc = 0, d = 0;
                 for (d = 0; d < 256; d++) {
@@ -537,10 +546,10 @@ __global__ void __launch_bounds__(256) k_crossing(Params P, const uint64_t *off2
                 s_sel[0] = d;
                 s_sel[1] = K - acc;
             }
-            __syncthreads();
+            block_sync();
             prefix |= s_sel[0] << sh;
             K = s_sel[1];
-            __syncthreads();
+            block_sync();
         }
         for (uint64_t q = e0 + threadIdx.x; q < e1; q += blockDim.x) {
             const uint64_t v = rec[q];
@@ -548,7 +557,7 @@ __global__ void __launch_bounds__(256) k_crossing(Params P, const uint64_t *off2
             const uint32_t j = (uint32_t)(v >> 32);
             if (j >= prefix) full_add(fullf, j);
         }
-        __syncthreads();
+        block_sync();
     }
 }
 

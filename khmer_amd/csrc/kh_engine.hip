@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -124,6 +125,49 @@ static void ws_prepare(Graph *g, const PassGeo &q) {
     }
 }
 
+// KH_CHECK (development): record buffers pre-filled with a sentinel; after
+// each scatter the slots still holding it (holes) are counted
+static bool check_mode() {
+    static bool v = [] { const char *e = getenv("KH_CHECK"); return e && atoi(e); }();
+    return v;
+}
+__global__ void k_count_sentinel(const uint64_t *r, uint64_t n, unsigned long long *out) {
+    unsigned long long c = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        c += r[i] == ~0ull;
+    c = wave_sum(c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+static void check_holes(Graph *g, const uint64_t *r, uint64_t n, const char *what) {
+    unsigned long long *d = nullptr, h = 0;
+    KH_HIP(hipMalloc((void **)&d, 8));
+    KH_HIP(hipMemsetAsync(d, 0, 8, g->stream));
+    hipLaunchKernelGGL(k_count_sentinel, dim3(4096), dim3(256), 0, g->stream, r, n, d);
+    KH_HIP(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, g->stream));
+    KH_HIP(hipStreamSynchronize(g->stream));
+    KH_HIP(hipFree(d));
+    if (h) {
+        fprintf(stderr, "KH_CHECK: %llu holes after %s (of %llu)\n", h, what, (unsigned long long)n);
+        std::vector<uint64_t> v(n);
+        KH_HIP(hipMemcpy(v.data(), r, n * 8, hipMemcpyDeviceToHost));
+        int shown = 0;
+        uint64_t run0 = 0, prev = ~0ull, runs = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            if (v[i] != ~0ull) continue;
+            if (i != prev + 1) {
+                if (shown < 12 && prev != ~0ull)
+                    fprintf(stderr, "  hole run [%llu, %llu) len %llu\n", (unsigned long long)run0,
+                            (unsigned long long)prev + 1, (unsigned long long)(prev + 1 - run0)), shown++;
+                run0 = i;
+                runs++;
+            }
+            prev = i;
+        }
+        fprintf(stderr, "  last run [%llu, %llu), %llu runs\n", (unsigned long long)run0, (unsigned long long)prev + 1,
+                (unsigned long long)runs);
+    }
+}
+
 // exclusive scan of n u32 counts into u64 offsets (rocPRIM decoupled look-back)
 static void scan_counts(Graph *g, const uint32_t *in, uint64_t *out, uint64_t n) {
     Workspace &w = g->ws;
@@ -206,19 +250,20 @@ static size_t lds_hist_l1(const Params &P, bool window) {
     return (size_t)((P.F1 + 3) & ~3u) * 4 + lds_window(window, L1_HIST_TILE);
 }
 // level-1 tail buffers (64 B per bucket) when they fit next to the tile
-static bool l1_tails(const Params &P) { return P.F1 <= 1024; }
+static int l1_seg(const Params &P) { return P.F1 <= 1024 ? 8 : 0; }
 static size_t lds_scatter_l1(const Params &P, bool window, int tile_kmers) {
     const size_t F1a = (P.F1 + 3) & ~3u;
-    return F1a * 8 + (size_t)L1_TILE_RECS * 8 + (l1_tails(P) ? F1a * 64 : 0) + F1a * 4 * 2 +
-           (size_t)L1_TILE_RECS * 2 + ((F1a + 7) & ~7u) + lds_window(window, tile_kmers);
+    return F1a * 8 + (size_t)L1_TILE_RECS * 8 + F1a * 8 * l1_seg(P) + F1a * 4 * 2 +
+           (size_t)L1_TILE_RECS * 2 + 64 + ((F1a + 7) & ~7u) + lds_window(window, tile_kmers);
 }
+constexpr int L2_SEG = 16;   // 128-B level-2 write segments
 static size_t lds_scatter_l2(const Params &P) {
     const size_t F2 = (size_t)1 << P.s2;
-    return F2 * 8 + (size_t)PT_TILE * 8 + F2 * 64 + F2 * 4 * 2 + F2;
+    return F2 * 8 + F2 * 8 * L2_SEG + F2 * 4 + F2;
 }
 static size_t lds_scatter_w(uint32_t FJ) {
     const size_t FJa = (FJ + 3) & ~3u;
-    return FJa * 8 + (size_t)PT_TILE * 4 + FJa * 32 + FJa * 4 * 2 + FJa;
+    return W_RPC * 8 + (W_RPC + 4) * 4 + FJa * 8 + (size_t)PT_TILE * 4 + FJa * 32 + FJa * 4 * 2 + 64 + FJa;
 }
 static size_t lds_apply(const Params &P) {
     const size_t R = (size_t)1 << P.s0;
@@ -246,6 +291,10 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
 
     KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
     if (bigc) KH_HIP(hipMemsetAsync(w.fullf, 0, flag_bytes, st));
+    if (check_mode()) {
+        KH_HIP(hipMemsetAsync(w.rec1, 0xFF, q.recs * 8, st));
+        KH_HIP(hipMemsetAsync(w.rec2, 0xFF, q.recs * 8, st));
+    }
 
     // level 1
     TIMED("hist_l1", hipLaunchKernelGGL(k_hist_l1<Src>, dim3(q.nch1), dim3(L1_THREADS), lds_hist_l1(P, window), st, P,
@@ -257,10 +306,11 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
         const int nt = std::min(L1_MAX_RPT, P.n - t0);
         const int kpt = std::max(1, L1_MAX_RPT / nt);
         const int tile_kmers = L1_THREADS * kpt;
-        auto kfn = l1_tails(P) ? k_scatter_l1<Src, true> : k_scatter_l1<Src, false>;
+        auto kfn = l1_seg(P) ? k_scatter_l1<Src, 8> : k_scatter_l1<Src, 0>;
         TIMED("scatter_l1", hipLaunchKernelGGL(kfn, dim3(q.nch1), dim3(L1_THREADS), lds_scatter_l1(P, window, tile_kmers),
                                                st, P, src, nkmers, q.ck1, q.nch1, kpt, t0, nt, w.moff, w.rec1));
     }
+    if (check_mode()) check_holes(g, w.rec1, q.recs, "scatter_l1");
     // level 2
     const unsigned g2 = (unsigned)q.nch2max;
     TIMED("hist_l2", hipLaunchKernelGGL(k_hist_l2, dim3(g2), dim3(PT_THREADS), F2 * 4, st, (uint32_t)F1, P.s0, P.s2,
@@ -268,9 +318,11 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
     TIMED("scan", scan_counts(g, w.mcnt, w.moff, F2 * q.nch2max));
     TIMED("off2", hipLaunchKernelGGL(k_off2, dim3((unsigned)std::min<uint64_t>((F1 * F2 + 255) / 256, 8192)),
                                      dim3(256), 0, st, (uint32_t)F1, P.s2, w.off1, w.ch2, w.moff, w.off2));
-    TIMED("scatter_l2", hipLaunchKernelGGL(k_scatter_l2, dim3(g2), dim3(PT_THREADS), lds_scatter_l2(P), st,
-                                           (uint32_t)F1, P.s0, P.s2, w.off1, w.ch2, w.moff, w.rec1, w.rec2));
+    TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2<PT_THREADS, L2_SEG>), dim3(g2), dim3(PT_THREADS),
+                                           lds_scatter_l2(P), st, (uint32_t)F1, P.s0, P.s2, w.off1, w.ch2, w.moff,
+                                           w.rec1, w.rec2));
 
+    if (check_mode()) check_holes(g, w.rec2, q.recs, "scatter_l2");
     // apply (winner segments -> first half of the dead level-1 buffer)
     uint32_t *win = (uint32_t *)w.rec1;
     uint32_t *wout = win + w.cap_recs;
@@ -306,8 +358,8 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
     TIMED("hist_w", hipLaunchKernelGGL(k_hist_w, dim3(q.nchw), dim3(PT_THREADS), wmeta + (size_t)q.FJ * 4, st, P, A,
                                        q.js, q.FJ, q.nchw, w.mcnt));
     TIMED("scan", scan_counts(g, w.mcnt, w.moff, (uint64_t)q.FJ * q.nchw));
-    TIMED("scatter_w", hipLaunchKernelGGL(k_scatter_w, dim3(q.nchw), dim3(PT_THREADS), wmeta + lds_scatter_w(q.FJ), st,
-                                          P, A, q.js, q.FJ, q.nchw, w.moff, wout));
+    TIMED("scatter_w", hipLaunchKernelGGL((k_scatter_w<PT_THREADS, 8>), dim3(q.nchw), dim3(PT_THREADS),
+                                          lds_scatter_w(q.FJ), st, P, A, q.js, q.FJ, q.nchw, w.moff, wout));
     TIMED("mark", hipLaunchKernelGGL(k_mark, dim3(q.FJ), dim3(PT_THREADS), ((size_t)1 << q.js) / 8, st, wout, w.moff,
                                      w.mcnt, q.nchw, q.FJ, q.js, w.ctr, want_new ? w.newbits : nullptr));
 
@@ -630,14 +682,16 @@ static void set_lds_limits() {
     (void)hipFuncSetAttribute((const void *)k_apply_count<BYTE>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_bit, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcTwoBit, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcBytes, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcHashes, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcTwoBit, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcBytes, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void *)k_scatter_l1<SrcHashes, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void *)k_scatter_l2, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void *)k_scatter_w, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+#define KH_LDS_MAX(...) (void)hipFuncSetAttribute((const void *)__VA_ARGS__, hipFuncAttributeMaxDynamicSharedMemorySize, lim)
+    KH_LDS_MAX(k_scatter_l1<SrcTwoBit, 0>);
+    KH_LDS_MAX(k_scatter_l1<SrcTwoBit, 8>);
+    KH_LDS_MAX(k_scatter_l1<SrcBytes, 0>);
+    KH_LDS_MAX(k_scatter_l1<SrcBytes, 8>);
+    KH_LDS_MAX(k_scatter_l1<SrcHashes, 0>);
+    KH_LDS_MAX(k_scatter_l1<SrcHashes, 8>);
+    KH_LDS_MAX((k_scatter_l2<PT_THREADS, L2_SEG>));
+    KH_LDS_MAX((k_scatter_w<PT_THREADS, 8>));
+#undef KH_LDS_MAX
     (void)hipFuncSetAttribute((const void *)k_mark, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipGetLastError();
 }
@@ -695,3 +749,10 @@ Graph::~Graph() {
 }
 
 }  // namespace kh
+
+extern "C" int kh_debug_read(uint64_t *out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kh::g_dbg), 64 * 8) != hipSuccess) return 5;
+    static const uint64_t z[64] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(kh::g_dbg), z, 64 * 8) != hipSuccess) return 5;
+    return 0;
+}

@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(Q_THREADS) k_kmer_hashes(Src src, uint64_t nkm
     const uint64_t j0 = (uint64_t)blockIdx.x * Q_TILE;
     const uint64_t j1 = min(nkmers, j0 + Q_TILE);
     TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
-    __syncthreads();
+    block_sync();
     for (uint64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) out[j] = kmer_hash(src, s_koff, tr, j);
 }
 
@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(Q_THREADS) k_kmer_counts(Params P, Src src, ui
     const uint64_t j0 = (uint64_t)blockIdx.x * Q_TILE;
     const uint64_t j1 = min(nkmers, j0 + Q_TILE);
     TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
-    __syncthreads();
+    block_sync();
     for (uint64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x)
         out[j] = (uint16_t)get_count_dev(P, tab, kmer_hash(src, s_koff, tr, j), bc_keys, bc_vals, bc_n);
 }

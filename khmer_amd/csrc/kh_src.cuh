@@ -12,6 +12,15 @@
 
 namespace kh {
 
+// Workgroup barrier with an explicit wait for this wave's LDS operations.
+// hipcc (ROCm 7.2, gfx950) was observed to emit a loop-header s_barrier with
+// no lgkmcnt wait on the back edge, so LDS stores at the end of one iteration
+// could land after other waves' LDS atomics of the next (lost counts).
+__device__ __forceinline__ void block_sync() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0), vmcnt/expcnt untouched
+    __syncthreads();
+}
+
 __device__ __forceinline__ uint64_t div_barrett(uint64_t x, uint64_t d, uint64_t m) {
     uint64_t q = umulhi64(x, m);
     return (x - q * d >= d) ? q + 1 : q;
@@ -79,11 +88,11 @@ __device__ __forceinline__ TileReads load_tile_reads(const Src &src, uint64_t j0
         s_meta[0] = lo;
         s_meta[1] = cnt;
     }
-    __syncthreads();
+    block_sync();
     tr.rlo = s_meta[0];
     tr.n = (uint32_t)s_meta[1];
     for (uint32_t t = threadIdx.x; t <= tr.n; t += blockDim.x) s_koff[t] = src.koff[tr.rlo + t];
-    __syncthreads();
+    block_sync();
     return tr;
 }
 
