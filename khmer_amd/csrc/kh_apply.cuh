@@ -145,6 +145,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
     uint32_t *full255 = s_wt + 16;        // [R/32] bins at 255 before the batch that got inserts
     uint32_t *s_flag = full255 + R / 32;  // [4]
     uint8_t *c0 = (uint8_t *)(s_flag + 4);  // [R]
+    uint8_t *wflag = c0 + R;              // [R/4] winner bits of each 4-bin group
     const uint32_t MAXC = KIND == BYTE ? 255u : 15u;
     const bool bigc = KIND == BYTE && P.use_bigcount;
     const uint32_t t = threadIdx.x;
@@ -152,6 +153,13 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
     const uint64_t total = A.rprefix[P.n];
     Prefetch cur, nxt;
     prefetch_region<KIND>(P, A, blockIdx.x, total, cur);
+#ifdef KH_PHASES
+    uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t tA = __builtin_amdgcn_s_memtime(), tB;
+#define PH(i) do { tB = __builtin_amdgcn_s_memtime(); ph[i] += tB - tA; tA = tB; } while (0)
+#else
+#define PH(i) do { } while (0)
+#endif
     for (uint64_t rr = blockIdx.x; rr < total; rr += gridDim.x) {
         const RegionInfo ri = cur.ri;
         if (ri.e0 == ri.e1) {
@@ -191,7 +199,9 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
             for (uint32_t x = t; x < R / 32; x += blockDim.x) full255[x] = 0;
             if (t == 0) s_flag[0] = 0;
         }
+        PH(5);
         block_sync();
+        PH(0);
         // records: the prefetched batch, then APPLY_RECS loads in flight per thread
         if (!(P.ablate & 2)) {
 #pragma unroll
@@ -209,44 +219,77 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
             }
         }
         block_sync();
-        prefetch_region<KIND>(P, A, rr + gridDim.x, total, nxt);
+        PH(1);
         // pass 1 (thread per bin, conflict-free LDS): winners (bins zero
         // before the batch keep their minimum k-mer index, the others drop
         // it), crossings, bins already full, saturated value into c0, changed
         // chunks
+        // pass 1, four consecutive bins per thread and step (one c0 word, one
+        // uint4 of counts): saturated values, winners (bins zero before the
+        // batch keep their minimum k-mer index; others drop it), crossings,
+        // bins already full, changed 16-bin chunks
         uint32_t nw = 0;
-#pragma unroll 2
-        for (int u = 0; u < BPT; u++) {
-            const uint32_t o = t + (uint32_t)u * APPLY_THREADS;
-            if (o >= nb) continue;
-            const uint32_t n = cnt[o];
-            if (!n) continue;
-            const uint32_t c = c0[o];
-            if (c == 0) {
-                nw++;
-                occ += (ri.i == 0);
-            } else {
-                minj[o] = NO_J;
+        const uint32_t lane = t & 63;
+#pragma unroll
+        for (int step = 0; step < BPT / 4; step++) {
+            const uint32_t g = t + (uint32_t)step * APPLY_THREADS;   // 4-bin group
+            const uint32_t o = 4 * g;
+            const uint4 n4 = ((const uint4 *)cnt)[g];
+            const uint32_t cw = ((const uint32_t *)c0)[g];
+            const uint32_t na[4] = {n4.x, n4.y, n4.z, n4.w};
+            uint32_t fw = cw, win = 0, inval = 0, full = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t n = o + k < nb ? na[k] : 0;
+                const uint32_t c = (cw >> (8 * k)) & 0xFFu;
+                if (!n) continue;
+                const uint32_t v = c + n;
+                const uint32_t f = v < MAXC ? v : MAXC;
+                fw = (fw & ~(0xFFu << (8 * k))) | (f << (8 * k));
+                if (c == 0) win |= 1u << k;
+                else inval |= 1u << k;
+                if (bigc && c == 255) full |= 1u << k;
+                if (bigc && c < 255 && v >= 255) {
+                    const uint64_t idx = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
+                    if (idx < A.cap_cross) A.cross[idx] = ((P.tbase[ri.i] + ri.bin_lo + o + k) << 8) | c;
+                    else atomicOr((unsigned long long *)&A.ctr[CTR_ERR], 1ull);
+                }
             }
-            if (bigc && c == 255) {
-                atomicOr(&full255[o >> 5], 1u << (o & 31));
+            const bool changed = fw != cw;
+            if (changed) ((uint32_t *)c0)[g] = fw;
+            if (inval) {
+                uint4 m = ((const uint4 *)minj)[g];
+                if (inval & 1) m.x = NO_J;
+                if (inval & 2) m.y = NO_J;
+                if (inval & 4) m.z = NO_J;
+                if (inval & 8) m.w = NO_J;
+                ((uint4 *)minj)[g] = m;
+            }
+            wflag[g] = (uint8_t)win;
+            const uint32_t pw = __popc(win);
+            nw += pw;
+            occ += ri.i == 0 ? pw : 0;
+            if (full) {
+                atomicOr(&full255[o >> 5], full << (o & 31));
                 s_flag[0] = 1;
             }
-            const uint32_t v = c + n;
-            if (bigc && c < 255 && v >= 255) {
-                const uint64_t idx = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
-                if (idx < A.cap_cross) A.cross[idx] = ((P.tbase[ri.i] + ri.bin_lo + o) << 8) | c;
-                else atomicOr((unsigned long long *)&A.ctr[CTR_ERR], 1ull);
-            }
-            const uint32_t f = v < MAXC ? v : MAXC;
-            if (f != c) {
-                c0[o] = (uint8_t)f;
-                atomicOr(&chg[o >> 9], 1u << ((o >> 4) & 31));
+            // changed 16-bin chunks: lanes 4c..4c+3 form chunk (g >> 2); one
+            // atomic per wave on chg word (g >> 7), bits (g >> 2) & 31
+            uint64_t m = __ballot(changed);
+            if (lane == 0 && m) {
+                m |= m >> 1;
+                m |= m >> 2;
+                uint32_t bits = 0;
+#pragma unroll
+                for (int c4 = 0; c4 < 16; c4++) bits |= (uint32_t)((m >> (4 * c4)) & 1) << c4;
+                atomicOr(&chg[g >> 7], bits << ((g >> 2) & 31));
             }
         }
         if (P.ablate & 1) nw = 0;
         const uint32_t wex = wave_winner_scan(nw, s_wt);
         block_sync();
+        PH(2);
+        prefetch_region<KIND>(P, A, rr + gridDim.x, total, nxt);
         // pass 2: write back changed 16-bin chunks; winners to the region's segment
         for (uint32_t x = t; x < nchunk; x += blockDim.x) {
             if (!((chg[x >> 5] >> (x & 31)) & 1) || (P.ablate & 4)) continue;
@@ -282,17 +325,28 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
         uint32_t wall;
         uint64_t pos = ri.e0 + winner_base(s_wt, &wall) + wex;
         if (nw) {
-#pragma unroll 2
-            for (int u = 0; u < BPT; u++) {
-                const uint32_t o = t + (uint32_t)u * APPLY_THREADS;
-                const uint32_t m = o < nb ? minj[o] : NO_J;
-                if (m != NO_J) A.win[pos++] = m;
+#pragma unroll
+            for (int step = 0; step < BPT / 4; step++) {
+                const uint32_t g = t + (uint32_t)step * APPLY_THREADS;
+                const uint32_t win = wflag[g];
+                if (!win) continue;
+                const uint4 m = ((const uint4 *)minj)[g];
+                if (win & 1) A.win[pos++] = m.x;
+                if (win & 2) A.win[pos++] = m.y;
+                if (win & 4) A.win[pos++] = m.z;
+                if (win & 8) A.win[pos++] = m.w;
             }
         }
         if (t == 0) A.wcnt[rr] = wall;
         block_sync();
+        PH(3);
         cur = nxt;
     }
+#ifdef KH_PHASES
+    if (threadIdx.x == 0)
+        for (int z = 0; z < 6; z++) atomicAdd(&g_dbg[16 + z], (unsigned long long)ph[z]);
+#endif
+#undef PH
     occ = wave_sum(occ);
     if ((threadIdx.x & 63) == 0 && occ) atomicAdd((unsigned long long *)&A.ctr[CTR_OCC], (unsigned long long)occ);
 }
@@ -343,18 +397,28 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyA
         prefetch_region<BIT>(P, A, rr + gridDim.x, total, nxt);
         // pass 1 (thread per bin): winners set their bit
         uint32_t nw = 0;
+        const uint32_t lane = t & 63;
 #pragma unroll 2
         for (int u = 0; u < BPT; u++) {
             const uint32_t o = t + (uint32_t)u * APPLY_THREADS;
-            if (o >= nb || minj[o] == NO_J) continue;
-            if ((bits[o >> 3] >> (o & 7)) & 1) {   // bit already set: not new
-                minj[o] = NO_J;
-                continue;
+            bool win = false;
+            if (o < nb && minj[o] != NO_J) {
+                if ((bits[o >> 3] >> (o & 7)) & 1) {   // bit already set: not new
+                    minj[o] = NO_J;
+                } else {
+                    win = true;
+                    nw++;
+                    occ += (ri.i == 0);
+                }
             }
-            atomicOr(&bits32[o >> 5], 1u << (o & 31));
-            atomicOr(&chg[o >> 12], 1u << ((o >> 7) & 31));
-            nw++;
-            occ += (ri.i == 0);
+            // a wave's 64 bins are two 32-bit words of the bit array and one
+            // 128-bin write-back chunk
+            const uint64_t m = __ballot(win);
+            if (m) {
+                if (lane == 0 && (uint32_t)m) atomicOr(&bits32[o >> 5], (uint32_t)m);
+                if (lane == 32 && (uint32_t)(m >> 32)) atomicOr(&bits32[o >> 5], (uint32_t)(m >> 32));
+                if (lane == 0) atomicOr(&chg[o >> 12], 1u << ((o >> 7) & 31));
+            }
         }
         const uint32_t wex = wave_winner_scan(nw, s_wt);
         block_sync();

@@ -267,7 +267,7 @@ static size_t lds_scatter_w(uint32_t FJ) {
 }
 static size_t lds_apply(const Params &P) {
     const size_t R = (size_t)1 << P.s0;
-    return P.kind == BIT ? R * 4 + 16 + 64 + R / 8 : R * 4 * 2 + (R / 512) * 4 + 64 + R / 8 + 16 + R;
+    return P.kind == BIT ? R * 4 + 16 + 64 + R / 8 : R * 4 * 2 + (R / 512) * 4 + 64 + R / 8 + 16 + R + R / 4;
 }
 
 // ---------------------------------------------------------------------------

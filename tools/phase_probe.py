@@ -25,4 +25,4 @@ for it in range(2):
     check(lib.kh_consume_packed_fixed_device(g._g, words, reads, L))
     check(lib.kh_device_synchronize(0))
     lib.kh_debug_read(dbg)
-    print("iter", it, "phases:", " ".join("%d:%.3e" % (i, dbg[i]) for i in range(16) if dbg[i]), flush=True)
+    print("iter", it, "phases:", " ".join("%d:%.3e" % (i, dbg[i]) for i in range(64) if dbg[i]), flush=True)

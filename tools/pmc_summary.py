@@ -1,0 +1,76 @@
+"""Summarise a tools/profile_round.sh run into profiles/.
+
+* profiles/<tag>_kernel_stats.csv : rocprofv3 --stats kernel summary (copied)
+* profiles/<tag>_bench.json       : the bench line measured under the tracer
+* profiles/<tag>_pmc.csv          : per-kernel HBM bytes per launch from the
+  FETCH_SIZE / WRITE_SIZE passes
+* profiles/pmc_traffic.json       : the dominant bench kernel's HBM bytes per
+  launch, read by bench.py for roofline.traffic
+
+Unit handling follows /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
+FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the
+bytes of wide coalesced streaming reads, so it is doubled.  Our record
+streams are 8-B-per-lane loads (not the guide's calibrated 16-B case), so the
+doubled value is an estimate; the raw counters are kept next to it.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+
+def counters(path):
+    agg = collections.defaultdict(lambda: [0, 0.0])
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            a = agg[name]
+            a[0] += 1
+            a[1] += float(r["Counter_Value"])
+    return agg
+
+
+def main():
+    out, tag = sys.argv[1], sys.argv[2]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = glob.glob(os.path.join(out, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(prof, "%s_kernel_stats.csv" % tag))
+    bench = json.load(open(os.path.join(out, "bench.json")))
+    json.dump(bench, open(os.path.join(prof, "%s_bench.json" % tag), "w"), indent=1)
+    fetch = counters(os.path.join(out, "pmc_FETCH_SIZE"))
+    write = counters(os.path.join(out, "pmc_WRITE_SIZE"))
+    rows = []
+    for name in sorted(set(fetch) | set(write)):
+        nf, f = fetch.get(name, [0, 0.0])
+        nw, w = write.get(name, [0, 0.0])
+        n = max(nf, nw, 1)
+        rows.append({"kernel": name, "launches": n,
+                     "fetch_kib_raw_per_launch": f / max(nf, 1),
+                     "write_kib_per_launch": w / max(nw, 1),
+                     "hbm_bytes_per_launch": (2.0 * f / max(nf, 1) + w / max(nw, 1)) * 1024.0})
+    with open(os.path.join(prof, "%s_pmc.csv" % tag), "w", newline="") as fh:
+        wr = csv.DictWriter(fh, fieldnames=list(rows[0]))
+        wr.writeheader()
+        wr.writerows(rows)
+    dom = bench["roofline"]["kernel"]
+    match = [r for r in rows if r["kernel"].split("<")[0].endswith("k_" + dom.split("_byte")[0].split("_nibble")[0].split("_bit")[0])
+             or r["kernel"].endswith(dom)]
+    if match:
+        r = match[0]
+        json.dump({"kernel": dom, "device_kernel": r["kernel"], "config": bench["config"]["workload"],
+                   "hbm_bytes_per_launch": r["hbm_bytes_per_launch"],
+                   "fetch_kib_raw_per_launch": r["fetch_kib_raw_per_launch"],
+                   "write_kib_per_launch": r["write_kib_per_launch"],
+                   "note": "FETCH_SIZE doubled per the gfx950 calibration; tag %s" % tag},
+                  open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+    print("dominant", dom, "match", match[:1])
+
+
+if __name__ == "__main__":
+    main()
