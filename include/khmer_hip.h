@@ -47,6 +47,7 @@ extern "C" {
 
 typedef struct kh_graph kh_graph;
 typedef struct kh_parser kh_parser;
+typedef struct kh_group kh_group;
 
 const char *kh_last_error(void);
 int kh_abi_version(void);
@@ -99,6 +100,9 @@ int  kh_graph_info(kh_graph *g, int *storage, int *hash_kind, int *k, int *n_tab
 int  kh_graph_tablesizes(kh_graph *g, uint64_t *out);          /* hashsizes() */
 int  kh_graph_set_use_bigcount(kh_graph *g, int on);           /* storage.cc:50-56 */
 int  kh_graph_get_use_bigcount(kh_graph *g, int *on);
+/* the bigcount map (storage.hh:498 KmerCountMap) sorted by hash: n entries
+ * are written when cap >= n; *n always receives the map size */
+int  kh_graph_get_bigcounts(kh_graph *g, uint64_t *keys, uint16_t *vals, uint64_t cap, uint64_t *n);
 int  kh_graph_n_unique_kmers(kh_graph *g, uint64_t *out);      /* storage.hh:143-165 */
 int  kh_graph_n_occupied(kh_graph *g, uint64_t *out);
 /* largest k-mer batch processed per device pipeline pass (memory knob) */
@@ -169,6 +173,33 @@ int kh_device_synchronize(int device);
  * stats are text lines "kernel<TAB>launches<TAB>total_ms" */
 int kh_graph_set_profiling(kh_graph *g, int on);
 int kh_graph_kernel_stats(kh_graph *g, char *buf, size_t cap, size_t *len);
+
+/* ---------------- multi-GPU sharded groups ----------------------------------
+ * SURVEY.md §8(e).  The reference has no multi-device path; its hash-space
+ * sharding precedent is k-mer banding (src/oxli/hashtable.cc:192-228), which
+ * yields byte-identical tables.  Here rank r of a G-rank group owns bins
+ * [lo_r, lo_{r+1}) of every table (contiguous, 8-bin aligned slices); input
+ * reads are consumed as one stream in rank order (source reads broadcast over
+ * RCCL/xGMI, each rank applies the updates of the bins it owns); n_unique,
+ * n_occupied and bigcounts are exact (winners routed to k-mer-window owners,
+ * bigcount tallies all-gathered).  One process per GPU (nlocal = 1, uid from
+ * rank 0's kh_group_unique_id), or all shards in one process on one device
+ * (nlocal = world, uid = NULL: loopback, for testing).  Consume calls are
+ * collective: every rank calls them in the same order with the same shape. */
+int kh_group_unique_id(unsigned char *out, size_t cap);   /* cap >= 128 */
+int kh_group_create(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables, int world, int rank,
+                    int nlocal, const int *devices, const unsigned char *uid, kh_group **out);
+void kh_group_destroy(kh_group *grp);
+/* local shard l as a graph handle (view: valid while the group lives; its
+ * tables are the slices [lo, lo + size) reported by kh_group_slice) */
+int kh_group_shard(kh_group *grp, int l, kh_graph **out);
+int kh_group_info(kh_group *grp, int *world, int *nlocal, int *rank0);
+int kh_group_slice(kh_group *grp, int l, int table, uint64_t *lo, uint64_t *size);
+/* replaces the per-rank consume loop (hashtable.cc:106-133) over 2-bit packed
+ * fixed-length reads: d_words[l] = local shard l's own reads (nlocal pointers) */
+int kh_group_consume_packed_fixed_device(kh_group *grp, const uint64_t *const *d_words, uint64_t nreads,
+                                         uint64_t read_len);
+int kh_group_counters(kh_group *grp, uint64_t *n_unique, uint64_t *n_occupied);   /* collective */
 
 #ifdef __cplusplus
 }

@@ -55,6 +55,15 @@ SIGNATURES = {
     "kh_graph_n_occupied": (i32, [P, PU64]),
     "kh_graph_set_batch_kmers": (i32, [P, u64]),
     "kh_graph_clear": (i32, [P]),
+    "kh_graph_get_bigcounts": (i32, [P, PU64, ctypes.POINTER(ctypes.c_uint16), u64, PU64]),
+    "kh_group_unique_id": (i32, [ctypes.c_char_p, sz]),
+    "kh_group_create": (i32, [i32, i32, i32, PU64, i32, i32, i32, i32, PI, ctypes.c_char_p, ctypes.POINTER(P)]),
+    "kh_group_destroy": (None, [P]),
+    "kh_group_shard": (i32, [P, i32, ctypes.POINTER(P)]),
+    "kh_group_info": (i32, [P, PI, PI, PI]),
+    "kh_group_slice": (i32, [P, i32, i32, PU64, PU64]),
+    "kh_group_consume_packed_fixed_device": (i32, [P, ctypes.POINTER(P), u64, u64]),
+    "kh_group_counters": (i32, [P, PU64, PU64]),
     "kh_consume_parser": (i32, [P, P, i32, PU32, PU64]),
     "kh_consume_seqs": (i32, [P, ctypes.c_char_p, PU64, u64, i32, PU64]),
     "kh_consume_packed_device": (i32, [P, P, P, u64, u64]),

@@ -54,7 +54,7 @@ __device__ __forceinline__ RegionInfo region_info(const Params &P, const ApplyAr
     ri.e0 = A.off2[region];
     ri.e1 = A.off2[region + 1];
     ri.bin_lo = lreg << P.s0;
-    ri.nb = (uint32_t)min((uint64_t)1 << P.s0, P.p[i] - ri.bin_lo);
+    ri.nb = (uint32_t)min((uint64_t)1 << P.s0, P.lsz[i] - ri.bin_lo);
     return ri;
 }
 
@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
                 if (c == 0) win |= 1u << k;
                 else inval |= 1u << k;
                 if (bigc && c == 255) full |= 1u << k;
-                if (bigc && c < 255 && v >= 255) {
+                if (bigc && c < 255 && v > 255) {   // insert r sees c + r: full iff c + r >= 255, r < n
                     const uint64_t idx = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
                     if (idx < A.cap_cross) A.cross[idx] = ((P.tbase[ri.i] + ri.bin_lo + o + k) << 8) | c;
                     else atomicOr((unsigned long long *)&A.ctr[CTR_ERR], 1ull);
@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(256) k_crossing(Params P, const uint64_t *off2
         const uint64_t region = G >> P.s0;
         const uint32_t o = (uint32_t)(G & rmask);
         const uint64_t e0 = off2[region], e1 = off2[region + 1];
-        uint32_t K = 255 - c0;          // rank of the first full insert
+        uint32_t K = 255 - c0;          // rank of the first full insert (< the bin's inserts: c0 + n > 255)
         uint32_t prefix = 0;
         for (int pass = 0; pass < 4; pass++) {
             const int sh = 24 - 8 * pass;
@@ -656,6 +656,69 @@ __global__ void __launch_bounds__(FIN_THREADS) k_finalize(Params P, Src src, uin
                 if (j < nkmers) out_hash[j] = kmer_hash_global(src, j);
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// sharded groups (kh_engine.hip group_*): winners of every shard are routed to
+// the rank owning their k-mer window; full events are merged on every rank
+
+// window start offsets of the partitioned winner list (FJ + 1 entries)
+__global__ void k_window_starts(const uint64_t *O3, const uint32_t *M3, uint32_t nchw, uint32_t FJ, uint64_t *ws) {
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w <= FJ; w += gridDim.x * blockDim.x) {
+        const uint64_t last = (uint64_t)FJ * nchw - 1;
+        ws[w] = w < FJ ? O3[(uint64_t)w * nchw] : O3[last] + M3[last];
+    }
+}
+
+// k_mark over windows [wlo, wlo + gridDim.x) whose winners arrived from G
+// shards: source s's part of window w is recv[roff[s] + ws_s[w] - ws_s[wlo] ...)
+__global__ void __launch_bounds__(PT_THREADS) k_mark_multi(const uint32_t *recv, const uint64_t *ws_all,
+                                                          const uint64_t *roff, int G, uint32_t FJ, uint32_t wlo,
+                                                          int js, uint64_t *ctr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *bits = (uint32_t *)smem;   // [2^js / 32]
+    const uint32_t nw = 1u << (js - 5);
+    const uint32_t w = wlo + blockIdx.x;
+    for (uint32_t t = threadIdx.x; t < nw / 4; t += blockDim.x) ((uint4 *)bits)[t] = make_uint4(0, 0, 0, 0);
+    block_sync();
+    const uint32_t mask = (1u << js) - 1;
+    for (int s = 0; s < G; s++) {
+        const uint64_t *ws = ws_all + (uint64_t)s * (FJ + 1);
+        const uint64_t b = roff[s] + (ws[w] - ws[wlo]);
+        const uint64_t n = ws[w + 1] - ws[w];
+        for (uint64_t q = threadIdx.x; q < n; q += blockDim.x) {
+            const uint32_t j = recv[b + q] & mask;
+            atomicOr(&bits[j >> 5], 1u << (j & 31));
+        }
+    }
+    block_sync();
+    uint64_t uniq = 0;
+    for (uint32_t t = threadIdx.x; t < nw / 4; t += blockDim.x) {
+        const uint4 x = ((const uint4 *)bits)[t];
+        uniq += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    }
+    uniq = wave_sum(uniq);
+    if ((threadIdx.x & 63) == 0 && uniq) atomicAdd((unsigned long long *)&ctr[CTR_UNIQUE], (unsigned long long)uniq);
+}
+
+// nonzero per-k-mer full tallies -> (j << 8 | tally) list (rare events)
+__global__ void k_full_compact(const uint8_t *fullf, uint64_t nkmers, uint64_t *list, uint64_t cap, uint64_t *ctr) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < nkmers; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t f = fullf[j];
+        if (!f) continue;
+        const uint64_t idx = atomicAdd((unsigned long long *)&ctr[CTR_NFULL], 1ull);
+        if (idx < cap) list[idx] = (j << 8) | f;   // overflow: the host sees NFULL > cap and retries
+    }
+}
+
+// add merged full tallies back into fullf (entries ~0 are padding)
+__global__ void k_full_scatter(const uint64_t *list, uint64_t n, uint8_t *fullf) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = list[i];
+        if (e == ~0ull) continue;
+        const uint32_t j = (uint32_t)(e >> 8);
+        atomicAdd((uint32_t *)(fullf + (j & ~3u)), (uint32_t)(e & 0xFF) << (8 * (j & 3u)));
     }
 }
 

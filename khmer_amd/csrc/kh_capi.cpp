@@ -32,7 +32,8 @@ void engine_synth_packed(int device, uint64_t seed, uint64_t r0, uint64_t nreads
 
 using namespace kh;
 
-struct kh_graph { Graph *g; };
+struct kh_graph { Graph *g; bool owned = true; };
+struct kh_group { ShardGroup *G; };
 struct kh_parser { Parser *p; };
 
 static thread_local std::string tl_err;
@@ -172,7 +173,7 @@ int kh_graph_create(int storage, int hash_kind, int k, const uint64_t *sizes, in
 
 void kh_graph_destroy(kh_graph *g) {
     if (!g) return;
-    delete g->g;
+    if (g->owned) delete g->g;
     delete g;
 }
 
@@ -819,5 +820,94 @@ extern "C" int kh_graph_clear(kh_graph *h) {
         g->bigcounts.clear();
         g->bc_dirty = true;
         g->tags.clear();
+    });
+}
+
+// ---------------------------------------------------------------------------
+// sharded groups
+extern "C" int kh_group_unique_id(unsigned char *out, size_t cap) {
+    return guard([&] {
+        CHECK_PTR(out);
+        group_unique_id(out, cap);
+    });
+}
+
+extern "C" int kh_group_create(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables, int world,
+                               int rank, int nlocal, const int *devices, const unsigned char *uid, kh_group **out) {
+    return guard([&] {
+        CHECK_PTR(sizes);
+        CHECK_PTR(devices);
+        CHECK_PTR(out);
+        *out = nullptr;
+        ShardGroup *G = group_create(storage, hash_kind, k, sizes, n_tables, world, rank, nlocal, devices, uid);
+        *out = new kh_group{G};
+    });
+}
+
+extern "C" void kh_group_destroy(kh_group *grp) {
+    if (!grp) return;
+    group_destroy(grp->G);
+    delete grp;
+}
+
+extern "C" int kh_group_shard(kh_group *grp, int l, kh_graph **out) {
+    return guard([&] {
+        CHECK_PTR(grp);
+        CHECK_PTR(out);
+        *out = new kh_graph{group_shard(grp->G, l), false};
+    });
+}
+
+extern "C" int kh_group_info(kh_group *grp, int *world, int *nlocal, int *rank0) {
+    return guard([&] {
+        CHECK_PTR(grp);
+        *world = group_world(grp->G);
+        *nlocal = group_nlocal(grp->G);
+        *rank0 = group_rank(grp->G, 0);
+    });
+}
+
+extern "C" int kh_group_slice(kh_group *grp, int l, int table, uint64_t *lo, uint64_t *size) {
+    return guard([&] {
+        CHECK_PTR(grp);
+        Graph *g = group_shard(grp->G, l);
+        if (table < 0 || table >= g->n) fail(KH_EVALUE, "no such table");
+        *lo = g->lo[(size_t)table];
+        *size = g->lsz[(size_t)table];
+    });
+}
+
+extern "C" int kh_group_consume_packed_fixed_device(kh_group *grp, const uint64_t *const *d_words, uint64_t nreads,
+                                                    uint64_t read_len) {
+    return guard([&] {
+        CHECK_PTR(grp);
+        CHECK_PTR(d_words);
+        std::vector<std::unique_lock<std::recursive_mutex>> locks;
+        for (int l = 0; l < group_nlocal(grp->G); l++) locks.emplace_back(group_shard(grp->G, l)->mu);
+        group_consume_fixed(grp->G, d_words, nreads, read_len);
+    });
+}
+
+extern "C" int kh_group_counters(kh_group *grp, uint64_t *n_unique, uint64_t *n_occupied) {
+    return guard([&] {
+        CHECK_PTR(grp);
+        group_counters(grp->G, n_unique, n_occupied);
+    });
+}
+
+extern "C" int kh_graph_get_bigcounts(kh_graph *h, uint64_t *keys, uint16_t *vals, uint64_t cap, uint64_t *n) {
+    return guard([&] {
+        CHECK_PTR(h);
+        CHECK_PTR(n);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        std::vector<std::pair<uint64_t, uint16_t>> v(g->bigcounts.begin(), g->bigcounts.end());
+        std::sort(v.begin(), v.end());
+        *n = v.size();
+        if (cap >= v.size() && keys && vals)
+            for (size_t i = 0; i < v.size(); i++) {
+                keys[i] = v[i].first;
+                vals[i] = v[i].second;
+            }
     });
 }

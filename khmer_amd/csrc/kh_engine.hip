@@ -71,7 +71,7 @@ static PassGeo pass_geo(const Params &P, uint64_t nkmers) {
     q.js = std::max(17, ceil_log2(nkmers) - 11);   // <= 2048 windows of <= 2^20 k-mers
     q.FJ = (uint32_t)((nkmers + (1ull << q.js) - 1) >> q.js);
     q.regions = 0;
-    for (int i = 0; i < P.n; i++) q.regions += (P.p[i] + (1ull << P.s0) - 1) >> P.s0;
+    for (int i = 0; i < P.n; i++) q.regions += (P.lsz[i] + (1ull << P.s0) - 1) >> P.s0;
     q.nchw = (uint32_t)((q.regions + W_RPC - 1) / W_RPC);
     const uint64_t F2 = 1ull << P.s2;
     q.mcnt = std::max<uint64_t>({(uint64_t)P.F1 * q.nch1, F2 * q.nch2max, (uint64_t)q.FJ * q.nchw});
@@ -272,17 +272,32 @@ static size_t lds_apply(const Params &P) {
 
 // ---------------------------------------------------------------------------
 // one device pass over a batch of <= 2^32 - 16 k-mers
+// A pass runs in three stages so a sharded group can exchange data between
+// them: (A) partition, apply, winner lists partitioned by k-mer window;
+// (B) mark: n_unique from the winners (+ per-k-mer new flags); (C) bigcount
+// candidates, per-k-mer outputs, counters.
+struct PassState {
+    PassGeo q;
+    uint64_t nkmers = 0;
+    bool bigc = false;
+    ApplyArgs A;
+    uint32_t *win = nullptr, *wout = nullptr;
+};
+
 template <class Src>
-static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *out) {
-    if (nkmers == 0) return;
+static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     if (nkmers > (1ull << 31)) fail(KH_EVALUE, "device batch too large (more than 2^31 k-mers)");
     const Params &P = g->prm;
-    const PassGeo q = pass_geo(P, nkmers);
+    PassState ps;
+    ps.q = pass_geo(P, nkmers);
+    ps.nkmers = nkmers;
+    const PassGeo &q = ps.q;
     ws_prepare(g, q);
     Workspace &w = g->ws;
     hipStream_t st = g->stream;
     const uint64_t F1 = P.F1, F2 = 1ull << P.s2;
     const bool bigc = P.kind == BYTE && P.use_bigcount;
+    ps.bigc = bigc;
     const bool window = [&] {
         if constexpr (!Src::kReads) return false;
         else return src.kpr == 0;
@@ -301,7 +316,7 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
                                         src, nkmers, q.ck1, q.nch1, w.mcnt));
     TIMED("scan", scan_counts(g, w.mcnt, w.moff, F1 * q.nch1));
     TIMED("plan_l2", hipLaunchKernelGGL(k_plan_l2, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1, q.nch1,
-                                        w.moff, q.recs, w.off1, w.ch2));
+                                        w.moff, w.mcnt, w.off1, w.ch2));
     for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
         const int nt = std::min(L1_MAX_RPT, P.n - t0);
         const int kpt = std::max(1, L1_MAX_RPT / nt);
@@ -326,7 +341,9 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
     // apply (winner segments -> first half of the dead level-1 buffer)
     uint32_t *win = (uint32_t *)w.rec1;
     uint32_t *wout = win + w.cap_recs;
-    ApplyArgs A;
+    ps.win = win;
+    ps.wout = wout;
+    ApplyArgs &A = ps.A;
     A.off2 = w.off2;
     A.rec = w.rec2;
     A.tab = g->d_tab;
@@ -338,7 +355,7 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
     A.ctr = w.ctr;
     A.rprefix[0] = 0;
     for (int i = 0; i < P.n; i++)
-        A.rprefix[i + 1] = A.rprefix[i] + ((P.p[i] + (1ull << P.s0) - 1) >> P.s0);
+        A.rprefix[i + 1] = A.rprefix[i] + ((P.lsz[i] + (1ull << P.s0) - 1) >> P.s0);
     const unsigned agrid = (unsigned)std::min<uint64_t>(q.regions, 256 * 2);
     if (P.kind == BIT)
         TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P), st, P, A));
@@ -352,17 +369,35 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
         TIMED("crossing", hipLaunchKernelGGL(k_crossing, dim3(1024), dim3(256), 0, st, P, w.off2, w.rec2, w.cross,
                                              w.ctr, w.cap_cross, w.fullf));
 
-    // winners -> k-mer windows -> n_unique (+ per-k-mer new flags)
-    const bool want_new = out && out->h_new;
+    // winners -> k-mer windows
     const size_t wmeta = W_RPC * 8 + (W_RPC + 4) * 4;
     TIMED("hist_w", hipLaunchKernelGGL(k_hist_w, dim3(q.nchw), dim3(PT_THREADS), wmeta + (size_t)q.FJ * 4, st, P, A,
                                        q.js, q.FJ, q.nchw, w.mcnt));
     TIMED("scan", scan_counts(g, w.mcnt, w.moff, (uint64_t)q.FJ * q.nchw));
     TIMED("scatter_w", hipLaunchKernelGGL((k_scatter_w<PT_THREADS, 8>), dim3(q.nchw), dim3(PT_THREADS),
                                           lds_scatter_w(q.FJ), st, P, A, q.js, q.FJ, q.nchw, w.moff, wout));
-    TIMED("mark", hipLaunchKernelGGL(k_mark, dim3(q.FJ), dim3(PT_THREADS), ((size_t)1 << q.js) / 8, st, wout, w.moff,
-                                     w.mcnt, q.nchw, q.FJ, q.js, w.ctr, want_new ? w.newbits : nullptr));
+    return ps;
+}
 
+// (B) one workgroup per window: LDS bitmap of its winners
+static void pass_mark_local(Graph *g, PassState &ps, bool want_new) {
+    Workspace &w = g->ws;
+    const PassGeo &q = ps.q;
+    hipStream_t st = g->stream;
+    TIMED("mark", hipLaunchKernelGGL(k_mark, dim3(q.FJ), dim3(PT_THREADS), ((size_t)1 << q.js) / 8, st, ps.wout,
+                                     w.moff, w.mcnt, q.nchw, q.FJ, q.js, w.ctr, want_new ? w.newbits : nullptr));
+}
+
+// (C) bigcount candidates (fullf complete), outputs, counters
+template <class Src>
+static void pass_stage_c(Graph *g, const Src &src, PassState &ps, const PassOut *out) {
+    Workspace &w = g->ws;
+    const Params &P = g->prm;
+    hipStream_t st = g->stream;
+    const uint64_t nkmers = ps.nkmers;
+    const bool bigc = ps.bigc;
+    const bool want_new = out && out->h_new;
+    const uint64_t flag_bytes = (nkmers + 15) & ~15ull;
     uint64_t *d_out_hash = nullptr;
     if (out && out->h_hash) d_out_hash = w.rec2;  // level-2 records are dead after crossing
     if (bigc || d_out_hash) {
@@ -404,6 +439,14 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
         }
         g->bc_dirty = true;
     }
+}
+
+template <class Src>
+static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *out) {
+    if (nkmers == 0) return;
+    PassState ps = pass_stage_a(g, src, nkmers);
+    pass_mark_local(g, ps, out && out->h_new);
+    pass_stage_c(g, src, ps, out);
 }
 
 // ---------------------------------------------------------------------------
@@ -655,21 +698,24 @@ void graph_prepare_params(Graph *g) {
     P.ablate = ab ? atoi(ab) : 0;
     P.s0 = g->kind == BIT ? 14 : 13;
     uint64_t maxreg = 1;
-    for (int i = 0; i < g->n; i++) maxreg = std::max<uint64_t>(maxreg, (g->sizes[i] + (1ull << P.s0) - 1) >> P.s0);
+    for (int i = 0; i < g->n; i++) maxreg = std::max<uint64_t>(maxreg, (g->lsz[i] + (1ull << P.s0) - 1) >> P.s0);
     P.s2 = std::min(10, ceil_log2(maxreg));
     const uint64_t span = 1ull << (P.s0 + P.s2);
     uint64_t base = 0, byteoff = 0;
     for (int i = 0; i < g->n; i++) {
         P.p[i] = g->sizes[i];
         P.m[i] = barrett_m(g->sizes[i]);
+        P.lo[i] = g->lo[i];
+        P.lsz[i] = g->lsz[i];
         P.tbase[i] = base;
-        base += (g->sizes[i] + span - 1) / span * span;
+        base += (g->lsz[i] + span - 1) / span * span;
         P.tbyte[i] = byteoff;
         P.tbytes[i] = g->nbytes[i];
         byteoff += (g->nbytes[i] + 255) / 256 * 256;
     }
     uint64_t F1 = base / span;
     if (F1 > 4096) fail(KH_EVALUE, "tables too large for one device (more than 4096 level-1 buckets)");
+    if (F1 == 0) F1 = 1;
     P.F1 = (uint32_t)F1;
 }
 
@@ -696,11 +742,12 @@ static void set_lds_limits() {
     (void)hipGetLastError();
 }
 
-Graph *graph_create(int kind, int hash, int k, const uint64_t *sizes, int n, int device) {
+Graph *graph_create_shard(int kind, int hash, int k, const uint64_t *sizes, int n, int device, int world, int rank) {
     if (n < 1 || n > MAXT) fail(KH_EVALUE, "number of tables must be in [1, 32]");
     if (kind != BYTE && kind != BIT && kind != NIBBLE) fail(KH_EVALUE, "unknown storage kind");
     if (hash == TWOBIT && (k < 1 || k > 32)) fail(KH_EVALUE, "k-mer size must be <= 32 for 2-bit hashing");
     if (hash == MURMUR && (k < 1 || k > 127)) fail(KH_EVALUE, "k-mer size must be in [1, 127]");
+    if (world < 1 || rank < 0 || rank >= world) fail(KH_EVALUE, "invalid shard rank / world size");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) fail(KH_EDEVICE, "no HIP device available");
     if (device < 0 || device >= ndev) fail(KH_EDEVICE, "invalid HIP device");
@@ -710,11 +757,19 @@ Graph *graph_create(int kind, int hash, int k, const uint64_t *sizes, int n, int
     g->k = k;
     g->n = n;
     g->device = device;
+    g->world = world;
+    g->rank = rank;
     for (int i = 0; i < n; i++) {
         if (sizes[i] == 0) fail(KH_EVALUE, "table size must be > 0");
         g->sizes.push_back(sizes[i]);
-        // storage.hh:127-140 (bit), 297-310 (nibble), 502-511 (byte)
-        g->nbytes.push_back(kind == BIT ? sizes[i] / 8 + 1 : kind == NIBBLE ? sizes[i] / 2 + 1 : sizes[i]);
+        // contiguous slices, 8-bin aligned so Bit/Nibble slices start on a byte
+        const uint64_t lo = shard_lo(sizes[i], world, rank), hi = shard_lo(sizes[i], world, rank + 1);
+        g->lo.push_back(lo);
+        g->lsz.push_back(hi - lo);
+        // storage.hh:127-140 (bit), 297-310 (nibble), 502-511 (byte); a slice
+        // carries the same trailing byte so the last shard matches the layout
+        const uint64_t m = hi - lo;
+        g->nbytes.push_back(kind == BIT ? m / 8 + 1 : kind == NIBBLE ? m / 2 + 1 : m);
     }
     KH_HIP(hipSetDevice(device));
     set_lds_limits();
@@ -732,6 +787,10 @@ Graph *graph_create(int kind, int hash, int k, const uint64_t *sizes, int n, int
     KH_HIP(hipMemsetAsync(g->d_tab, 0, arena, g->stream));
     KH_HIP(hipStreamSynchronize(g->stream));
     return g.release();
+}
+
+Graph *graph_create(int kind, int hash, int k, const uint64_t *sizes, int n, int device) {
+    return graph_create_shard(kind, hash, k, sizes, n, device, 1, 0);
 }
 
 Graph::~Graph() {
@@ -756,3 +815,334 @@ extern "C" int kh_debug_read(uint64_t *out) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(kh::g_dbg), z, 64 * 8) != hipSuccess) return 5;
     return 0;
 }
+
+// ===========================================================================
+// Sharded groups ("read broadcast + owner-computes", exact):
+// rank r of a G-rank group holds bins [lo_r, lo_r+1) of every table (8-bin
+// aligned contiguous slices).  Input reads are consumed in rank order as ONE
+// global stream: source s's packed reads are broadcast (RCCL over xGMI) and
+// every rank hashes every k-mer but keeps only the (k-mer, table) records of
+// bins it owns, so each table byte is updated exactly as on one device.  The
+// order-dependent counters stay exact: winners (first inserters of zero bins)
+// are routed to the rank owning their k-mer window, which ORs all shards'
+// winners in an LDS bitmap; bigcount "full" tallies (rare) are all-gathered
+// and summed on every rank, so the bigcount map is replicated.
+// Loopback mode runs all G shards in one process on one device (device
+// copies instead of RCCL), which is how the protocol is tested on one GPU.
+#include <rccl/rccl.h>
+
+namespace kh {
+
+#define KH_NCCL(x)                                                                                    \
+    do {                                                                                              \
+        ncclResult_t r_ = (x);                                                                        \
+        if (r_ != ncclSuccess) fail(KH_EDEVICE, std::string("RCCL: ") + ncclGetErrorString(r_));     \
+    } while (0)
+
+struct ShardGroup {
+    int world = 1, rank0 = 0, nlocal = 1;
+    std::vector<Graph *> shards;
+    ncclComm_t comm = nullptr;
+    struct Local {
+        uint64_t *src = nullptr;
+        uint64_t cap_src = 0;        // broadcast reads of another rank (RCCL)
+        uint32_t *recv = nullptr;
+        uint64_t cap_recv = 0;       // winners routed to this rank
+        uint64_t *ws = nullptr;
+        uint64_t cap_ws = 0;         // own window starts
+        uint64_t *ws_all = nullptr;
+        uint64_t cap_ws_all = 0;     // every shard's window starts
+        uint64_t *roff = nullptr;
+        uint64_t cap_roff = 0;
+        uint64_t *flist = nullptr;
+        uint64_t cap_flist = 0;      // own full-tally list
+        uint64_t *fall = nullptr;
+        uint64_t cap_fall = 0;       // gathered full-tally lists
+    };
+    std::vector<Local> loc;
+    uint64_t *d_red = nullptr;
+    std::vector<uint64_t> h_ws;      // [G][FJ+1]
+    ~ShardGroup() {
+        for (size_t l = 0; l < loc.size(); l++) {
+            (void)hipSetDevice(shards[l]->device);
+            for (void *p : {(void *)loc[l].src, (void *)loc[l].recv, (void *)loc[l].ws, (void *)loc[l].ws_all,
+                            (void *)loc[l].roff, (void *)loc[l].flist, (void *)loc[l].fall})
+                if (p) (void)hipFree(p);
+        }
+        if (d_red) (void)hipFree(d_red);
+        if (comm) (void)ncclCommDestroy(comm);
+        for (Graph *g : shards) delete g;
+    }
+};
+
+constexpr uint64_t FULL_LIST_CAP = 1ull << 24;
+
+void group_unique_id(unsigned char *out, size_t n) {
+    ncclUniqueId id;
+    if (n < sizeof id) fail(KH_EVALUE, "unique id buffer too small");
+    KH_NCCL(ncclGetUniqueId(&id));
+    memcpy(out, &id, sizeof id);
+}
+
+ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank, int nlocal,
+                         const int *devices, const unsigned char *uid) {
+    if (world < 1 || world > 64) fail(KH_EVALUE, "group size must be in [1, 64]");
+    if (nlocal != 1 && nlocal != world) fail(KH_EVALUE, "a process holds one shard (RCCL) or all shards (loopback)");
+    if (nlocal == 1 && (rank < 0 || rank >= world)) fail(KH_EVALUE, "invalid rank");
+    std::unique_ptr<ShardGroup> G(new ShardGroup());
+    G->world = world;
+    G->nlocal = nlocal;
+    G->rank0 = nlocal == world ? 0 : rank;
+    for (int l = 0; l < nlocal; l++)
+        G->shards.push_back(graph_create_shard(kind, hash, k, sizes, n, devices[l], world, G->rank0 + l));
+    G->loc.resize(nlocal);
+    if (nlocal == 1 && world > 1) {
+        if (!uid) fail(KH_EVALUE, "an RCCL group needs the unique id of rank 0");
+        ncclUniqueId id;
+        memcpy(&id, uid, sizeof id);
+        KH_HIP(hipSetDevice(devices[0]));
+        KH_NCCL(ncclCommInitRank(&G->comm, world, id, rank));
+        KH_HIP(hipMalloc((void **)&G->d_red, 256 * 8));   // [0,64) gathers, [128,..) scalars
+    }
+    return G.release();
+}
+
+void group_destroy(ShardGroup *G) { delete G; }
+
+static uint32_t group_wlo(uint32_t FJ, int W, int r) { return (uint32_t)((uint64_t)FJ * (uint64_t)r / (uint64_t)W); }
+
+// winners of every shard -> window owners -> LDS-bitmap union (n_unique partials)
+static void group_route_winners(ShardGroup *G, std::vector<PassState> &ps) {
+    const int W = G->world, NL = G->nlocal;
+    const uint32_t FJ = ps[0].q.FJ;
+    const int js = ps[0].q.js;
+    for (int l = 0; l < NL; l++) {
+        Graph *g = G->shards[l];
+        auto &lc = G->loc[l];
+        KH_HIP(hipSetDevice(g->device));
+        ensure((void **)&lc.ws, &lc.cap_ws, FJ + 1, 8);
+        ensure((void **)&lc.ws_all, &lc.cap_ws_all, (uint64_t)W * (FJ + 1), 8);
+        ensure((void **)&lc.roff, &lc.cap_roff, W, 8);
+        TIMED("route", hipLaunchKernelGGL(k_window_starts, dim3((FJ + 256) / 256), dim3(256), 0, g->stream,
+                                          g->ws.moff, g->ws.mcnt, ps[l].q.nchw, FJ, lc.ws));
+    }
+    G->h_ws.assign((size_t)W * (FJ + 1), 0);
+    if (G->comm) {
+        Graph *g = G->shards[0];
+        auto &lc = G->loc[0];
+        KH_NCCL(ncclAllGather(lc.ws, lc.ws_all, FJ + 1, ncclUint64, G->comm, g->stream));
+        KH_HIP(hipMemcpyAsync(G->h_ws.data(), lc.ws_all, G->h_ws.size() * 8, hipMemcpyDeviceToHost, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+    } else {
+        for (int s = 0; s < NL; s++) {
+            KH_HIP(hipSetDevice(G->shards[s]->device));
+            KH_HIP(hipMemcpyAsync(G->h_ws.data() + (size_t)s * (FJ + 1), G->loc[s].ws, (FJ + 1) * 8,
+                                  hipMemcpyDeviceToHost, G->shards[s]->stream));
+        }
+        for (int s = 0; s < NL; s++) KH_HIP(hipStreamSynchronize(G->shards[s]->stream));
+        for (int l = 0; l < NL; l++)
+            KH_HIP(hipMemcpy(G->loc[l].ws_all, G->h_ws.data(), G->h_ws.size() * 8, hipMemcpyHostToDevice));
+    }
+    auto wsv = [&](int s, uint32_t w) { return G->h_ws[(size_t)s * (FJ + 1) + w]; };
+    for (int l = 0; l < NL; l++) {
+        const int r = G->rank0 + l;
+        Graph *g = G->shards[l];
+        auto &lc = G->loc[l];
+        KH_HIP(hipSetDevice(g->device));
+        const uint32_t wl = group_wlo(FJ, W, r), wh = group_wlo(FJ, W, r + 1);
+        std::vector<uint64_t> roff(W);
+        uint64_t tot = 0;
+        for (int s = 0; s < W; s++) {
+            roff[s] = tot;
+            tot += wsv(s, wh) - wsv(s, wl);
+        }
+        ensure((void **)&lc.recv, &lc.cap_recv, tot + 1, 4);
+        KH_HIP(hipMemcpyAsync(lc.roff, roff.data(), W * 8, hipMemcpyHostToDevice, g->stream));
+        if (G->comm) {
+            // own part first (device copy), then the grouped point-to-point exchange
+            const uint64_t own = wsv(r, wh) - wsv(r, wl);
+            if (own)
+                KH_HIP(hipMemcpyAsync(lc.recv + roff[r], ps[0].wout + wsv(r, wl), own * 4, hipMemcpyDeviceToDevice,
+                                      g->stream));
+            KH_NCCL(ncclGroupStart());
+            for (int d = 0; d < W; d++) {
+                if (d == r) continue;
+                const uint64_t c = wsv(r, group_wlo(FJ, W, d + 1)) - wsv(r, group_wlo(FJ, W, d));
+                if (c)
+                    KH_NCCL(ncclSend(ps[0].wout + wsv(r, group_wlo(FJ, W, d)), c, ncclUint32, d, G->comm,
+                                     g->stream));
+                const uint64_t cin = wsv(d, wh) - wsv(d, wl);
+                if (cin) KH_NCCL(ncclRecv(lc.recv + roff[d], cin, ncclUint32, d, G->comm, g->stream));
+            }
+            KH_NCCL(ncclGroupEnd());
+        } else {
+            for (int s = 0; s < W; s++) {
+                const uint64_t c = wsv(s, wh) - wsv(s, wl);
+                if (c)
+                    KH_HIP(hipMemcpyAsync(lc.recv + roff[s], ps[s].wout + wsv(s, wl), c * 4, hipMemcpyDeviceToDevice,
+                                          g->stream));
+            }
+        }
+        if (wh > wl)
+            TIMED("mark", hipLaunchKernelGGL(k_mark_multi, dim3(wh - wl), dim3(PT_THREADS), ((size_t)1 << js) / 8,
+                                             g->stream, lc.recv, lc.ws_all, lc.roff, W, FJ, wl, js, g->ws.ctr));
+    }
+}
+
+// bigcount: per-k-mer full tallies of all shards summed on every rank
+static void group_merge_full(ShardGroup *G, std::vector<PassState> &ps) {
+    const int W = G->world, NL = G->nlocal;
+    const uint64_t nk = ps[0].nkmers;
+    std::vector<uint64_t> cnt(W, 0);
+    for (int l = 0; l < NL; l++) {
+        Graph *g = G->shards[l];
+        auto &lc = G->loc[l];
+        KH_HIP(hipSetDevice(g->device));
+        ensure((void **)&lc.flist, &lc.cap_flist, 1024, 8);
+        const uint64_t cap = std::min<uint64_t>(FULL_LIST_CAP, lc.cap_flist);
+        hipLaunchKernelGGL(k_full_compact, dim3(2048), dim3(256), 0, g->stream, g->ws.fullf, nk, lc.flist, cap,
+                           g->ws.ctr);
+        uint64_t h[CTR_N];
+        KH_HIP(hipMemcpyAsync(h, g->ws.ctr, CTR_N * 8, hipMemcpyDeviceToHost, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+        if (h[CTR_NFULL] > cap) {
+            // grow once and recompute (bounded by FULL_LIST_CAP)
+            if (h[CTR_NFULL] > FULL_LIST_CAP)
+                fail(KH_EDEVICE, "too many bigcount events in one sharded batch; lower the batch size");
+            ensure((void **)&lc.flist, &lc.cap_flist, h[CTR_NFULL], 8);
+            KH_HIP(hipMemsetAsync(g->ws.ctr + CTR_NFULL, 0, 8, g->stream));
+            hipLaunchKernelGGL(k_full_compact, dim3(2048), dim3(256), 0, g->stream, g->ws.fullf, nk, lc.flist,
+                               lc.cap_flist, g->ws.ctr);
+            KH_HIP(hipStreamSynchronize(g->stream));
+        }
+        cnt[G->rank0 + l] = h[CTR_NFULL];
+    }
+    if (G->comm) {
+        Graph *g = G->shards[0];
+        auto &lc = G->loc[0];
+        KH_HIP(hipMemcpyAsync(G->d_red + 128, &cnt[G->rank0], 8, hipMemcpyHostToDevice, g->stream));
+        KH_NCCL(ncclAllGather(G->d_red + 128, G->d_red, 1, ncclUint64, G->comm, g->stream));
+        KH_HIP(hipMemcpyAsync(cnt.data(), G->d_red, W * 8, hipMemcpyDeviceToHost, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+        const uint64_t mx = *std::max_element(cnt.begin(), cnt.end());
+        if (!mx) return;
+        ensure((void **)&lc.flist, &lc.cap_flist, mx, 8);
+        if (mx > cnt[G->rank0])
+            KH_HIP(hipMemsetAsync(lc.flist + cnt[G->rank0], 0xFF, (mx - cnt[G->rank0]) * 8, g->stream));
+        ensure((void **)&lc.fall, &lc.cap_fall, (uint64_t)W * mx, 8);
+        KH_NCCL(ncclAllGather(lc.flist, lc.fall, mx, ncclUint64, G->comm, g->stream));
+        KH_HIP(hipMemsetAsync(g->ws.fullf, 0, (nk + 15) & ~15ull, g->stream));
+        hipLaunchKernelGGL(k_full_scatter, dim3(2048), dim3(256), 0, g->stream, lc.fall, (uint64_t)W * mx,
+                           g->ws.fullf);
+    } else {
+        uint64_t any = 0;
+        for (uint64_t c : cnt) any |= c;
+        if (!any) return;
+        for (int l = 0; l < NL; l++) {
+            Graph *g = G->shards[l];
+            KH_HIP(hipSetDevice(g->device));
+            KH_HIP(hipMemsetAsync(g->ws.fullf, 0, (nk + 15) & ~15ull, g->stream));
+            for (int s = 0; s < W; s++)
+                if (cnt[s])
+                    hipLaunchKernelGGL(k_full_scatter, dim3(2048), dim3(256), 0, g->stream, G->loc[s].flist, cnt[s],
+                                       g->ws.fullf);
+        }
+    }
+    KH_HIP(hipGetLastError());
+}
+
+// collective: every rank passes its own fixed-length packed reads (same
+// count and length on every rank); consumed as the stream rank 0, 1, ...
+void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len) {
+    const int W = G->world, NL = G->nlocal;
+    Graph *g0 = G->shards[0];
+    const int k = g0->k;
+    if (g0->hash != TWOBIT) fail(KH_EVALUE, "sharded consume takes 2-bit packed reads");
+    if (read_len < (uint64_t)k) fail(KH_EVALUE, "reads shorter than k");
+    if (G->comm) {
+        // every rank must pass the same shape (collective schedule depends on it)
+        uint64_t h[2] = {nreads, read_len};
+        KH_HIP(hipSetDevice(g0->device));
+        KH_HIP(hipMemcpyAsync(G->d_red + 140, h, 16, hipMemcpyHostToDevice, g0->stream));
+        KH_NCCL(ncclAllReduce(G->d_red + 140, G->d_red + 142, 2, ncclUint64, ncclMax, G->comm, g0->stream));
+        KH_NCCL(ncclAllReduce(G->d_red + 140, G->d_red + 144, 2, ncclUint64, ncclMin, G->comm, g0->stream));
+        uint64_t mm[4];
+        KH_HIP(hipMemcpyAsync(mm, G->d_red + 142, 32, hipMemcpyDeviceToHost, g0->stream));
+        KH_HIP(hipStreamSynchronize(g0->stream));
+        if (mm[0] != mm[2] || mm[1] != mm[3]) fail(KH_EVALUE, "ranks passed different read counts or lengths");
+    }
+    const uint64_t kpr = read_len - k + 1;
+    const uint64_t nwords = (nreads * read_len + 31) / 32 + 1;
+    const uint64_t rpb = std::max<uint64_t>(1, std::min<uint64_t>(g0->batch_kmers, 1ull << 31) / kpr);
+    for (int s = 0; s < W; s++) {
+        std::vector<const uint64_t *> buf(NL);
+        if (G->comm) {
+            auto &lc = G->loc[0];
+            KH_HIP(hipSetDevice(g0->device));
+            uint64_t *dst;
+            if (G->rank0 == s) {
+                dst = const_cast<uint64_t *>(d_words[0]);
+            } else {
+                ensure((void **)&lc.src, &lc.cap_src, nwords, 8);
+                dst = lc.src;
+            }
+            Graph *g = g0;
+            TIMED("bcast", KH_NCCL(ncclBroadcast(dst, dst, nwords, ncclUint64, s, G->comm, g->stream)));
+            buf[0] = dst;
+        } else {
+            for (int l = 0; l < NL; l++) buf[l] = d_words[s];
+        }
+        for (uint64_t r0 = 0; r0 < nreads; r0 += rpb) {
+            const uint64_t nr = std::min(rpb, nreads - r0);
+            std::vector<PassState> ps(NL);
+            std::vector<SrcTwoBit> srcs(NL);
+            for (int l = 0; l < NL; l++) {
+                Graph *g = G->shards[l];
+                KH_HIP(hipSetDevice(g->device));
+                SrcTwoBit sb = src_twobit(g, buf[l]);
+                set_fixed(sb, kpr);
+                sb.koff = nullptr;
+                sb.nreads = nr;
+                sb.kbase = r0 * kpr;
+                sb.rbase = 0;
+                srcs[l] = sb;
+                ps[l] = pass_stage_a(g, sb, nr * kpr);
+            }
+            group_route_winners(G, ps);
+            if (ps[0].bigc) group_merge_full(G, ps);
+            for (int l = 0; l < NL; l++) {
+                KH_HIP(hipSetDevice(G->shards[l]->device));
+                pass_stage_c(G->shards[l], srcs[l], ps[l], nullptr);
+            }
+        }
+    }
+}
+
+// n_unique / n_occupied of the whole group (collective in RCCL mode)
+void group_counters(ShardGroup *G, uint64_t *n_unique, uint64_t *n_occupied) {
+    uint64_t h[2] = {0, 0};
+    for (Graph *g : G->shards) {
+        h[0] += g->n_unique;
+        h[1] += g->n_occupied;
+    }
+    if (G->comm) {
+        Graph *g = G->shards[0];
+        KH_HIP(hipSetDevice(g->device));
+        KH_HIP(hipMemcpyAsync(G->d_red + 150, h, 16, hipMemcpyHostToDevice, g->stream));
+        KH_NCCL(ncclAllReduce(G->d_red + 150, G->d_red + 152, 2, ncclUint64, ncclSum, G->comm, g->stream));
+        KH_HIP(hipMemcpyAsync(h, G->d_red + 152, 16, hipMemcpyDeviceToHost, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+    }
+    *n_unique = h[0];
+    *n_occupied = h[1];
+}
+
+int group_world(ShardGroup *G) { return G->world; }
+int group_nlocal(ShardGroup *G) { return G->nlocal; }
+int group_rank(ShardGroup *G, int l) { return G->rank0 + l; }
+Graph *group_shard(ShardGroup *G, int l) {
+    if (l < 0 || l >= G->nlocal) fail(KH_EVALUE, "no such local shard");
+    return G->shards[l];
+}
+
+}  // namespace kh

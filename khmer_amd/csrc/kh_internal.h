@@ -55,7 +55,9 @@ struct Params {
     uint32_t F1;
     int use_bigcount;
     int ablate;               // timing-only ablation bits (KH_ABLATE env); 0 in normal use
-    uint64_t p[MAXT];         // table sizes (bins)
+    uint64_t p[MAXT];         // table sizes (bins) -- the primes the hash is reduced by
+    uint64_t lo[MAXT];        // first bin of table i held here (0 unless sharded)
+    uint64_t lsz[MAXT];       // bins of table i held here (p[i] unless sharded)
     uint64_t m[MAXT];         // Barrett constants
     uint64_t tbase[MAXT];     // global bin base of table i
     uint64_t tbyte[MAXT];     // byte offset of table i in the table arena
@@ -91,11 +93,15 @@ struct Workspace {
     uint16_t *q_counts = nullptr;
     uint64_t cap_q = 0, cap_q16 = 0;
 };
-enum { CTR_OCC = 0, CTR_UNIQUE, CTR_NCROSS, CTR_NBC, CTR_ERR, CTR_N };
+enum { CTR_OCC = 0, CTR_UNIQUE, CTR_NCROSS, CTR_NBC, CTR_ERR, CTR_NFULL, CTR_N };
 
 struct Graph {
     int kind = BYTE, hash = TWOBIT, k = 0, n = 0, device = 0;
     std::vector<uint64_t> sizes, nbytes;
+    // shard of a multi-GPU group: this graph holds bins [lo, lo + lsz) of every
+    // table (lo = 0, lsz = sizes when not sharded); nbytes are the slice's bytes
+    int world = 1, rank = 0;
+    std::vector<uint64_t> lo, lsz;
     Geometry geo;
     Params prm;
     uint8_t *d_tab = nullptr;         // table arena
@@ -161,6 +167,13 @@ struct ReadView {
 
 // ---- engine (kh_engine.hip) ----
 Graph *graph_create(int kind, int hash, int k, const uint64_t *sizes, int n, int device);
+Graph *graph_create_shard(int kind, int hash, int k, const uint64_t *sizes, int n, int device, int world, int rank);
+// first bin of shard r of a p-bin table split over `world` shards (8-aligned)
+inline uint64_t shard_lo(uint64_t p, int world, int r) {
+    if (r >= world) return p;
+    const uint64_t x = (uint64_t)(((unsigned __int128)p * (unsigned)r) / (unsigned)world);
+    return x & ~7ull;
+}
 void graph_zero_counters(Graph *g);
 void graph_prepare_params(Graph *g);
 // run one device pipeline pass over a device-resident batch.
@@ -184,5 +197,18 @@ void engine_sync_bigcounts(Graph *g);
 void engine_download_table(Graph *g, int i, uint8_t *dst);
 void engine_upload_table(Graph *g, int i, const uint8_t *src);
 void engine_collect_events(Graph *g);
+
+// ---- sharded groups (kh_engine.hip) ----
+struct ShardGroup;
+void group_unique_id(unsigned char *out, size_t n);
+ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank, int nlocal,
+                         const int *devices, const unsigned char *uid);
+void group_destroy(ShardGroup *G);
+void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len);
+void group_counters(ShardGroup *G, uint64_t *n_unique, uint64_t *n_occupied);
+int group_world(ShardGroup *G);
+int group_nlocal(ShardGroup *G);
+int group_rank(ShardGroup *G, int l);
+Graph *group_shard(ShardGroup *G, int l);
 
 }  // namespace kh

@@ -206,7 +206,10 @@ __global__ void __launch_bounds__(L1_THREADS) k_hist_l1(Params P, Src src, uint6
         TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
         for (uint64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
             const uint64_t h = kmer_hash(src, s_koff, tr, j);
-            for (int i = 0; i < P.n; i++) atomicAdd(&hist[global_bin(P, i, h) >> shift], 1u);
+            for (int i = 0; i < P.n; i++) {
+                uint64_t G;
+                if (local_bin(P, i, h, &G)) atomicAdd(&hist[G >> shift], 1u);
+            }
         }
     }
     block_sync();
@@ -215,11 +218,14 @@ __global__ void __launch_bounds__(L1_THREADS) k_hist_l1(Params P, Src src, uint6
 
 // level-1 bucket offsets (from the scanned matrix) and the level-2 chunk
 // prefix: bucket b owns level-2 chunks [ch2[b], ch2[b+1])
-__global__ void __launch_bounds__(1024) k_plan_l2(uint32_t F1, uint32_t nch1, const uint64_t *O1, uint64_t total,
+__global__ void __launch_bounds__(1024) k_plan_l2(uint32_t F1, uint32_t nch1, const uint64_t *O1, const uint32_t *M1,
                                                   uint64_t *off1, uint32_t *ch2) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t *v = (uint64_t *)smem;   // [F1]
     uint64_t *s_part = v + F1;        // [1025]
+    // records of this pass (only the owned ones when sharded)
+    const uint64_t last = (uint64_t)F1 * nch1 - 1;
+    const uint64_t total = O1[last] + M1[last];
     for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) {
         const uint64_t s = O1[(uint64_t)b * nch1];
         const uint64_t e = b + 1 < F1 ? O1[(uint64_t)(b + 1) * nch1] : total;
@@ -294,7 +300,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
         uint32_t jj[L1_MAX_RPT];
         int nr = 0;
 #pragma unroll
-        for (int q = 0; q < L1_MAX_RPT; q++) { G[q] = 0; rank[q] = 0; jj[q] = 0; }
+        for (int q = 0; q < L1_MAX_RPT; q++) { G[q] = ~0ull; rank[q] = 0; jj[q] = 0; }
         // pass A: hashes (all input loads in flight), bins, tile histogram (ranks)
         if (!pre) {
 #pragma unroll
@@ -311,10 +317,15 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
             for (int q = 0; q < L1_MAX_RPT; q++) {
                 const int i = q - a * nt;  // table slot of register q for k-mer a
                 if (ok && i >= 0 && i < nt) {
-                    G[q] = global_bin(P, t0 + i, hh[a]);
-                    jj[q] = (uint32_t)j;
-                    rank[q] = atomicAdd(&hist[(uint32_t)(G[q] >> shift)], 1u);
-                    nr = q + 1;
+                    uint64_t Gq;
+                    if (local_bin(P, t0 + i, hh[a], &Gq)) {   // owned here
+                        G[q] = Gq;
+                        jj[q] = (uint32_t)j;
+                        rank[q] = atomicAdd(&hist[(uint32_t)(Gq >> shift)], 1u);
+                        nr = q + 1;
+                    } else {
+                        G[q] = ~0ull;
+                    }
                 }
             }
         }
@@ -326,7 +337,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
         // pass B: place in LDS in bucket order
 #pragma unroll
         for (int q = 0; q < L1_MAX_RPT; q++) {
-            if (q < nr) {
+            if (q < nr && G[q] != ~0ull) {
                 const uint32_t b = (uint32_t)(G[q] >> shift);
                 const uint32_t pos = lstart[b] + rank[q];
                 stage[pos] = ((uint64_t)jj[q] << 32) | (G[q] & omask);
@@ -346,7 +357,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
         block_sync();
         PH(3);
         // pass C: whole segments at the chunk's cursors
-        const uint32_t nrec = (uint32_t)((j1 - j0) * (uint64_t)nt);
+        const uint32_t nrec = lstart[F1 - 1] + hist[F1 - 1];   // records staged (owned ones)
 #pragma unroll
         for (int u = 0; u < L1_MAX_RPT; u++) {
             const uint32_t q = threadIdx.x + (uint32_t)u * L1_THREADS;

@@ -141,8 +141,12 @@ __device__ __forceinline__ uint64_t kmer_hash_global(const Src &src, uint64_t j)
     }
 }
 
-__device__ __forceinline__ uint64_t global_bin(const Params &P, int i, uint64_t h) {
-    return P.tbase[i] + mod_barrett(h, P.p[i], P.m[i]);
+// bin of hash h in table i (h mod p_i, storage.hh:577) as a bin of the local
+// bin space (table bases P.tbase); false when another shard owns it
+__device__ __forceinline__ bool local_bin(const Params &P, int i, uint64_t h, uint64_t *G) {
+    const uint64_t b = mod_barrett(h, P.p[i], P.m[i]) - P.lo[i];
+    *G = P.tbase[i] + b;
+    return b < P.lsz[i];
 }
 
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {

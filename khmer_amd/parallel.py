@@ -1,0 +1,245 @@
+"""Multi-GPU sharded Countgraph/Nodegraph.
+
+The reference has no multi-device path; its own hash-space sharding
+precedent is k-mer banding (src/oxli/hashtable.cc:192-228,
+src/oxli/kmer_hash.cc:262-276), which yields byte-identical tables.  Here a
+G-rank group splits every table by bin ownership: rank r holds the contiguous,
+8-bin aligned slice [shard_lo(p, G, r), shard_lo(p, G, r + 1)) of each table
+(the reference's table layout is recovered by concatenating the slices,
+`reinterleave`).  Reads are consumed as one stream in rank order: each source
+rank's packed reads are broadcast over RCCL (xGMI), every rank hashes every
+k-mer and applies only the updates of the bins it owns (owner-computes), so
+the tables are exactly the single-device tables.  n_unique / n_occupied /
+bigcounts stay exact (see include/khmer_hip.h, kh_group_*).
+
+Process model: one process per GPU under torchrun; torch.distributed (gloo)
+only carries the RCCL unique id, barriers and the max-over-ranks timing; the
+data path is the library's own RCCL communicator.  `loopback=True` runs all
+shards in one process on one device (device copies instead of RCCL), which is
+how the protocol is exercised on a one-GPU box.
+"""
+import ctypes
+
+from . import _lib
+from ._lib import lib, check
+
+KIND = {"Countgraph": _lib.STORAGE_BYTE, "Nodegraph": _lib.STORAGE_BIT, "SmallCountgraph": _lib.STORAGE_NIBBLE}
+
+
+def shard_lo(p, world, r):
+    """First bin of shard r of a p-bin table (kh_internal.h shard_lo)."""
+    if r >= world:
+        return p
+    return (p * r // world) & ~7
+
+
+def shard_slices(sizes, world):
+    """[(lo, size)] per rank per table."""
+    return [[(shard_lo(p, world, r), shard_lo(p, world, r + 1) - shard_lo(p, world, r)) for p in sizes]
+            for r in range(world)]
+
+
+def reinterleave(kind, p, parts):
+    """Table bytes of a p-bin table from its rank slices (in rank order).
+    Non-final Bit/Nibble slices are whole bytes followed by one spare byte."""
+    out = bytearray()
+    world = len(parts)
+    for r, part in enumerate(parts):
+        size = shard_lo(p, world, r + 1) - shard_lo(p, world, r)
+        if kind == _lib.STORAGE_BIT:
+            n = size // 8 + (1 if r == world - 1 else 0)
+        elif kind == _lib.STORAGE_NIBBLE:
+            n = size // 2 + (1 if r == world - 1 else 0)
+        else:
+            n = size
+        out += bytes(part[:n])
+    return bytes(out)
+
+
+def window_owner_range(fj, world, r):
+    """k-mer windows [lo, hi) whose winners rank r unions (kh_engine.hip group_wlo)."""
+    return fj * r // world, fj * (r + 1) // world
+
+
+class _ShardView(object):
+    """Non-owning handle of one local shard (kh_group_shard)."""
+
+    def __init__(self, handle):
+        self._g = handle
+
+    def __del__(self):
+        if self._g:
+            lib.kh_graph_destroy(self._g)
+            self._g = None
+
+    def bigcounts(self):
+        n = ctypes.c_uint64()
+        check(lib.kh_graph_get_bigcounts(self._g, None, None, 0, ctypes.byref(n)))
+        keys = (ctypes.c_uint64 * max(n.value, 1))()
+        vals = (ctypes.c_uint16 * max(n.value, 1))()
+        check(lib.kh_graph_get_bigcounts(self._g, keys, vals, n.value, ctypes.byref(n)))
+        return list(zip(keys[:n.value], vals[:n.value]))
+
+    def table_bytes(self, i):
+        n = ctypes.c_uint64()
+        check(lib.kh_graph_table_nbytes(self._g, i, ctypes.byref(n)))
+        buf = (ctypes.c_uint8 * max(n.value, 1))()
+        check(lib.kh_graph_copy_table(self._g, i, buf))
+        return bytes(buf[:n.value])
+
+
+class ShardedGraph(object):
+    """A Countgraph/Nodegraph/SmallCountgraph split over `world` ranks."""
+
+    def __init__(self, cls, k, sizes, world, rank=0, device=0, loopback=False, uid=None):
+        self.kind = KIND[cls]
+        self.k, self.sizes, self.world = k, [int(x) for x in sizes], world
+        self.loopback = loopback
+        nlocal = world if loopback else 1
+        devs = (ctypes.c_int * nlocal)(*([device] * nlocal))
+        arr = (ctypes.c_uint64 * len(sizes))(*self.sizes)
+        h = ctypes.c_void_p()
+        check(lib.kh_group_create(self.kind, _lib.HASH_TWOBIT, k, arr, len(sizes), world, rank, nlocal, devs,
+                                  uid, ctypes.byref(h)))
+        self._h = h
+        w, nl, r0 = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib.kh_group_info(h, ctypes.byref(w), ctypes.byref(nl), ctypes.byref(r0)))
+        self.nlocal, self.rank0 = nl.value, r0.value
+        self.shards = []
+        for l in range(self.nlocal):
+            v = ctypes.c_void_p()
+            check(lib.kh_group_shard(h, l, ctypes.byref(v)))
+            self.shards.append(_ShardView(v))
+
+    def close(self):
+        self.shards = []
+        if self._h:
+            lib.kh_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(128)
+        check(lib.kh_group_unique_id(buf, 128))
+        return buf.raw
+
+    def slice(self, l, table):
+        lo, n = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib.kh_group_slice(self._h, l, table, ctypes.byref(lo), ctypes.byref(n)))
+        return lo.value, n.value
+
+    def set_use_bigcount(self, flag):
+        for s in self.shards:
+            check(lib.kh_graph_set_use_bigcount(s._g, 1 if flag else 0))
+
+    def set_batch_kmers(self, n):
+        for s in self.shards:
+            check(lib.kh_graph_set_batch_kmers(s._g, int(n)))
+
+    def set_profiling(self, on):
+        for s in self.shards:
+            check(lib.kh_graph_set_profiling(s._g, 1 if on else 0))
+
+    def clear(self):
+        for s in self.shards:
+            check(lib.kh_graph_clear(s._g))
+
+    def consume_packed_fixed_device(self, d_words, nreads, read_len):
+        """Collective: d_words = one device pointer per local shard (its own reads)."""
+        ptrs = (ctypes.c_void_p * len(d_words))(*[int(p) if not isinstance(p, ctypes.c_void_p) else p.value
+                                                   for p in d_words])
+        check(lib.kh_group_consume_packed_fixed_device(self._h, ptrs, int(nreads), int(read_len)))
+
+    def counters(self):
+        """(n_unique_kmers, n_occupied) of the whole group (collective)."""
+        u, o = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib.kh_group_counters(self._h, ctypes.byref(u), ctypes.byref(o)))
+        return u.value, o.value
+
+    def local_tables(self):
+        """[[slice bytes per table] per local shard]."""
+        return [[s.table_bytes(i) for i in range(len(self.sizes))] for s in self.shards]
+
+    def gather_tables(self, all_gather=None):
+        """Reference-layout table bytes of the whole group.  Loopback: from the
+        local shards; one-process-per-rank: `all_gather(obj) -> [obj per rank]`
+        (e.g. a torch.distributed gloo all_gather_object wrapper)."""
+        parts = self.local_tables()
+        if not self.loopback:
+            parts = [p[0] for p in all_gather(parts)]
+        return [reinterleave(self.kind, p, [parts[r][i] for r in range(self.world)])
+                for i, p in enumerate(self.sizes)]
+
+
+class ShardedCountgraphBench(object):
+    """bench.py runner for --gpus N > 1 (one process per GPU, torchrun)."""
+
+    def __init__(self, args, rank, world, local, sizes):
+        self.args, self.rank, self.world, self.device, self.sizes = args, rank, world, local, sizes
+
+    def config_name(self):
+        a = self.args
+        return "Countgraph k=%d %dx%.0e sharded over %dxMI355X, %d x %d bp synthetic reads per GPU" % (
+            a.k, a.tables, a.x, self.world, a.reads, a.read_len)
+
+    def setup(self):
+        import torch.distributed as dist
+        from . import synth
+        a = self.args
+        if not dist.is_initialized():
+            dist.init_process_group("gloo")
+        self.dist = dist
+        obj = [ShardedGraph.unique_id() if self.rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        self.g = ShardedGraph("Countgraph", a.k, self.sizes, self.world, self.rank, self.device, uid=obj[0])
+        self.g.set_use_bigcount(not a.no_bigcount)
+        self.g.set_batch_kmers(a.batch_kmers)
+        nwords = a.reads * a.read_len // 32 + 2
+        self.words, self.koff = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib.kh_device_malloc(self.device, nwords * 8, ctypes.byref(self.words)))
+        check(lib.kh_device_malloc(self.device, (a.reads + 1) * 8, ctypes.byref(self.koff)))
+        # every rank's own reads: the rank-th block of the synthetic stream
+        check(lib.kh_synth_packed_device(self.device, synth.SEED, self.rank * a.reads, a.reads, a.read_len, a.k,
+                                         self.words, self.koff))
+
+    def step(self):
+        self.g.clear()
+        self.g.consume_packed_fixed_device([self.words], self.args.reads, self.args.read_len)
+
+    def sync(self):
+        check(lib.kh_device_synchronize(self.device))
+
+    def barrier(self):
+        self.dist.barrier()
+
+    def max_over_ranks(self, t):
+        import torch
+        x = torch.tensor([t], dtype=torch.float64)
+        self.dist.all_reduce(x, op=self.dist.ReduceOp.MAX)
+        return float(x.item())
+
+    def profile(self, on):
+        self.g.set_profiling(on)
+
+    def kernel_stats(self):
+        buf = ctypes.create_string_buffer(1 << 16)
+        n = ctypes.c_size_t()
+        check(lib.kh_graph_kernel_stats(self.g.shards[0]._g, buf, len(buf), ctypes.byref(n)))
+        out = {}
+        for line in buf.value.decode().splitlines():
+            name, cnt, ms = line.split("\t")
+            out[name] = (int(cnt), float(ms))
+        return out
+
+    def check(self):
+        u, o = self.g.counters()
+        return {"n_unique_kmers": u, "n_occupied": o}
+
+    def close(self):
+        lib.kh_device_free(self.device, self.words)
+        lib.kh_device_free(self.device, self.koff)
+        self.g.close()
+

@@ -266,3 +266,43 @@ def test_variable_length_reads_multi_batch(tmp_path):
         lib.kh_graph_set_batch_kmers(g._g, 20000)
         assert g.consume_seqfile(path) == o.consume_fastx(path)
         assert_same(g, o, "ragged " + cls)
+
+
+@pytest.mark.parametrize("batch", [1 << 27, 100000, 50000])
+@pytest.mark.parametrize("path", ["fixed", "variable"])
+def test_multibatch_saturated_bigcount(path, batch):
+    """Tables saturated over several device batches: bins entering a batch at
+    254 - n .. 255 exercise the crossing rule exactly (an insert is full iff
+    it sees 255; a bin reaching exactly 255 has no full insert)."""
+    import ctypes
+    from khmer_amd._lib import lib, check
+    sizes = O.get_n_primes_near_x(4, 3001)
+    R, L, k = 10000, 150, 21
+    o = O.Table(O.BYTE, k, sizes)
+    o.set_use_bigcount(True)
+    seqs, offs = synth.batch(0, R, L)
+    o.consume_batch(seqs, [int(v) for v in offs])
+    g = khmer.Countgraph(k, 1, 1, primes=sizes)
+    g.set_use_bigcount(True)
+    check(lib.kh_graph_set_batch_kmers(g._g, batch))
+    words, koff = ctypes.c_void_p(), ctypes.c_void_p()
+    check(lib.kh_device_malloc(0, (R * L // 32 + 2) * 8, ctypes.byref(words)))
+    check(lib.kh_device_malloc(0, (R + 1) * 8, ctypes.byref(koff)))
+    try:
+        check(lib.kh_synth_packed_device(0, synth.SEED, 0, R, L, k, words, koff))
+        if path == "fixed":
+            check(lib.kh_consume_packed_fixed_device(g._g, words, R, L))
+        else:
+            check(lib.kh_consume_packed_device(g._g, words, koff, R, R * (L - k + 1)))
+    finally:
+        lib.kh_device_free(0, words)
+        lib.kh_device_free(0, koff)
+    assert_same(g, o, "saturated %s %d" % (path, batch))
+    n = ctypes.c_uint64()
+    check(lib.kh_graph_get_bigcounts(g._g, None, None, 0, ctypes.byref(n)))
+    keys = (ctypes.c_uint64 * n.value)()
+    vals = (ctypes.c_uint16 * n.value)()
+    check(lib.kh_graph_get_bigcounts(g._g, keys, vals, n.value, ctypes.byref(n)))
+    assert dict(zip(keys, vals)) == o.bigcounts()
+    assert len(o.bigcounts()) > 1000
+    assert (g.n_unique_kmers(), g.n_occupied()) == (o.n_unique_kmers(), o.n_occupied())

@@ -1,0 +1,91 @@
+"""Sharded multi-GPU protocol (khmer_amd.parallel, kh_group_*) against the
+oracle.  On a one-GPU box the G shards run in loopback mode (one process, one
+device, device copies where the RCCL build sends over xGMI); the kernels, the
+ownership filter, the winner routing and the bigcount merge are the ones the
+one-process-per-GPU path runs.  Reads of source rank s are the s-th block of
+the synthetic stream, consumed in rank order, so the oracle consumes the
+concatenation."""
+import ctypes
+
+import pytest
+
+from oracle import oracle as O
+
+khmer = pytest.importorskip("khmer_amd")
+from khmer_amd import parallel, synth  # noqa: E402
+from khmer_amd._lib import lib, check  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+KIND = {"Countgraph": O.BYTE, "Nodegraph": O.BIT, "SmallCountgraph": O.NIBBLE}
+
+
+class DeviceReads(object):
+    def __init__(self, r0, nreads, L, k):
+        self.words, self.koff = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib.kh_device_malloc(0, (nreads * L // 32 + 2) * 8, ctypes.byref(self.words)))
+        check(lib.kh_device_malloc(0, (nreads + 1) * 8, ctypes.byref(self.koff)))
+        check(lib.kh_synth_packed_device(0, synth.SEED, r0, nreads, L, k, self.words, self.koff))
+
+    def __del__(self):
+        lib.kh_device_free(0, self.words)
+        lib.kh_device_free(0, self.koff)
+
+
+def run_pair(cls, k, sizes, world, nreads, L, batch, bigcount):
+    g = parallel.ShardedGraph(cls, k, sizes, world, loopback=True)
+    g.set_batch_kmers(batch)
+    o = O.Table(KIND[cls], k, sizes)
+    if bigcount:
+        g.set_use_bigcount(True)
+        o.set_use_bigcount(True)
+    srcs = [DeviceReads(s * nreads, nreads, L, k) for s in range(world)]
+    g.consume_packed_fixed_device([s.words for s in srcs], nreads, L)
+    for s in range(world):
+        seqs, offs = synth.batch(s * nreads, nreads, L)
+        o.consume_batch(seqs, [int(v) for v in offs])
+    return g, o
+
+
+def assert_group_equals_oracle(g, o, sizes, bigcount):
+    tabs = g.gather_tables()
+    for i in range(len(sizes)):
+        assert tabs[i] == o.table_bytes(i), "table %d" % i
+    u, occ = g.counters()
+    assert (u, occ) == (o.n_unique_kmers(), o.n_occupied())
+    if bigcount:
+        ref = sorted(o.bigcounts().items())
+        for sh in g.shards:   # replicated on every rank
+            assert sh.bigcounts() == ref
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("cls,k", [("Countgraph", 21), ("Nodegraph", 31), ("SmallCountgraph", 21)])
+def test_loopback_group_matches_oracle(cls, k, world):
+    sizes = O.get_n_primes_near_x(4, 200003)
+    g, o = run_pair(cls, k, sizes, world, nreads=4000, L=150, batch=1 << 17, bigcount=(cls == "Countgraph"))
+    assert_group_equals_oracle(g, o, sizes, cls == "Countgraph")
+    g.close()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_loopback_group_saturated_bigcount(world):
+    """Tiny tables: most bins saturate, so crossings, full tallies and the
+    all-gathered bigcount merge all run, across several batches per source."""
+    sizes = O.get_n_primes_near_x(4, 3001)
+    g, o = run_pair("Countgraph", 21, sizes, world, nreads=12000 // world, L=150, batch=100000, bigcount=True)
+    assert len(o.bigcounts()) > 100
+    assert_group_equals_oracle(g, o, sizes, True)
+    g.close()
+
+
+def test_group_slices_cover_tables():
+    sizes = [1000003, 999983, 7, 65]
+    g = parallel.ShardedGraph("Nodegraph", 31, sizes, 5, loopback=True)
+    for i, p in enumerate(sizes):
+        los = [g.slice(l, i) for l in range(5)]
+        assert los[0][0] == 0 and sum(n for _, n in los) == p
+        for l in range(4):
+            assert los[l][0] + los[l][1] == los[l + 1][0] and los[l + 1][0] % 8 == 0
+        assert [g.slice(l, i) for l in range(5)] == [parallel.shard_slices(sizes, 5)[l][i] for l in range(5)]
+    g.close()
