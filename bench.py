@@ -100,6 +100,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # development only: put every rank on one device (exercising RCCL on a one-GPU box)
+    local = int(os.environ.get("KH_BENCH_DEVICE", local))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
 

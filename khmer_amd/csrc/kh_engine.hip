@@ -1026,7 +1026,16 @@ static void group_merge_full(ShardGroup *G, std::vector<PassState> &ps) {
         KH_HIP(hipStreamSynchronize(g->stream));
         const uint64_t mx = *std::max_element(cnt.begin(), cnt.end());
         if (!mx) return;
-        ensure((void **)&lc.flist, &lc.cap_flist, mx, 8);
+        if (mx > lc.cap_flist) {   // grow keeping the compacted entries
+            uint64_t *nl = nullptr;
+            KH_HIP(hipMalloc((void **)&nl, mx * 8 + 64));
+            if (cnt[G->rank0])
+                KH_HIP(hipMemcpyAsync(nl, lc.flist, cnt[G->rank0] * 8, hipMemcpyDeviceToDevice, g->stream));
+            KH_HIP(hipStreamSynchronize(g->stream));
+            KH_HIP(hipFree(lc.flist));
+            lc.flist = nl;
+            lc.cap_flist = mx;
+        }
         if (mx > cnt[G->rank0])
             KH_HIP(hipMemsetAsync(lc.flist + cnt[G->rank0], 0xFF, (mx - cnt[G->rank0]) * 8, g->stream));
         ensure((void **)&lc.fall, &lc.cap_fall, (uint64_t)W * mx, 8);

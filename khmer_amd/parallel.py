@@ -92,6 +92,8 @@ class ShardedGraph(object):
     """A Countgraph/Nodegraph/SmallCountgraph split over `world` ranks."""
 
     def __init__(self, cls, k, sizes, world, rank=0, device=0, loopback=False, uid=None):
+        self._h = None
+        self.shards = []
         self.kind = KIND[cls]
         self.k, self.sizes, self.world = k, [int(x) for x in sizes], world
         self.loopback = loopback
