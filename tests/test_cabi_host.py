@@ -107,6 +107,62 @@ def test_parser_matches_oracle(fname):
     assert ours == theirs
 
 
+BZ2_FILES = ["100-reads.fq.bz2", "random-20-a.fa.bz2", "random-20-a.fq.bz2", "test-abund-read-2.fa.bz2"]
+
+
+def _decompressed(tmp_path, fname):
+    import bz2
+    out = tmp_path / fname.replace(".bz2", "")
+    out.write_bytes(bz2.decompress(open(data(fname), "rb").read()))
+    return str(out)
+
+
+@pytest.mark.parametrize("fname", BZ2_FILES)
+def test_parser_bzip2(tmp_path, fname):
+    """bzip2 input (seqan autodetection, reference tests/test_read_parsers.py:208-215):
+    the records equal the oracle's on Python's bz2-decompressed copy."""
+    ours = [(r.name, r.sequence, getattr(r, "quality", "")) for r in khmer.ReadParser(data(fname))]
+    assert ours == list(O.read_fastx(_decompressed(tmp_path, fname)))
+    if fname == "100-reads.fq.bz2":
+        assert len(ours) == 100
+
+
+def test_parser_bzip2_multistream(tmp_path):
+    import bz2
+    raw = open(data("random-20-a.fq"), "rb").read()
+    cut = raw.index(b"@", len(raw) // 2)
+    f = tmp_path / "multi.fq.bz2"
+    f.write_bytes(bz2.compress(raw[:cut]) + bz2.compress(raw[cut:]))
+    ours = [(r.name, r.sequence, r.quality) for r in khmer.ReadParser(str(f))]
+    assert ours == list(O.read_fastx(data("random-20-a.fq")))
+
+
+@pytest.mark.parametrize("fname", ["100-reads.fq.truncated.bz2", "100-reads.fq.truncated.gz"])
+def test_parser_truncated_compressed(fname):
+    """Opening succeeds; iterating raises OSError (reference
+    tests/test_read_parsers.py:183-228)."""
+    p = khmer.ReadParser(data(fname))
+    with pytest.raises(OSError):
+        for _ in p:
+            pass
+
+
+@pytest.mark.parametrize("fname", ["test-empty.fa.bz2", "empty-file.bz2"])
+def test_parser_empty_bzip2(fname):
+    with pytest.raises(OSError, match="does not contain any sequences"):
+        khmer.ReadParser(data(fname))
+
+
+def test_parser_corrupt_bzip2(tmp_path):
+    import bz2
+    blob = bytearray(bz2.compress(open(data("random-20-a.fa"), "rb").read()))
+    blob[len(blob) // 2] ^= 0xFF
+    f = tmp_path / "corrupt.fa.bz2"
+    f.write_bytes(bytes(blob))
+    with pytest.raises(OSError):
+        list(khmer.ReadParser(str(f)))
+
+
 def test_parser_errors(tmp_path):
     p = khmer.ReadParser(data("truncated.fq"))
     n = 0

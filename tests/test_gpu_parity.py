@@ -64,6 +64,27 @@ def test_fixture_consume(cls, fname, k, x, n):
         assert g.n_unique_kmers() == o.n_unique_kmers()
 
 
+@pytest.mark.parametrize("cls", ["Countgraph", "SmallCountgraph", "Nodegraph"])
+@pytest.mark.parametrize("fname", ["100-reads.fq.bz2", "random-20-a.fq.bz2", "test-abund-read-2.fa.bz2"])
+def test_bzip2_consume(tmp_path, cls, fname):
+    """bzip2 input straight to the device; the oracle reads Python's
+    bz2-decompressed copy."""
+    import bz2
+    plain = tmp_path / fname[:-4]
+    plain.write_bytes(bz2.decompress(open(data(fname), "rb").read()))
+    sizes = O.get_n_primes_near_x(4, 100003)
+    g, o = make_pair(cls, 20, sizes, bigcount=(cls == "Countgraph"))
+    assert g.consume_seqfile(data(fname)) == o.consume_fastx(str(plain))
+    assert_same(g, o, "%s %s" % (cls, fname))
+
+
+@pytest.mark.parametrize("fname", ["100-reads.fq.truncated.bz2", "100-reads.fq.truncated.gz"])
+def test_truncated_compressed_consume_raises(fname):
+    g = khmer.Countgraph(20, 1e5, 4)
+    with pytest.raises(OSError):
+        g.consume_seqfile(data(fname))
+
+
 @pytest.mark.parametrize("cls", ["Counttable", "SmallCounttable", "Nodetable"])
 @pytest.mark.parametrize("fname", ["random-20-a.fa", "test-abund-read-2.fa", "valid-read-testing.fq"])
 @pytest.mark.parametrize("k", [4, 15, 51])

@@ -189,3 +189,19 @@ def test_script_entry_points(tmp_path):
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "Total number of unique k-mers: 3960" in r.stderr, r.stderr
     assert os.path.exists(out + ".tagset")
+
+
+@pytest.mark.parametrize("suffix", [".gz", ".bz2"])
+def test_load_into_counting_compressed(tmp_path, capsys, suffix):
+    """Compressed inputs give the same table as the plain file."""
+    src = data("test-abund-read-2.fa" + suffix) if suffix == ".bz2" else None
+    if src is None:
+        import gzip
+        src = str(tmp_path / "in.fa.gz")
+        with open(ABUND, "rb") as fi, gzip.open(src, "wb") as fo:
+            fo.write(fi.read())
+    out = str(tmp_path / "out.ct")
+    st, _, err = run(S.load_into_counting, ["-x", "1e3", "-N", "2", "-k", "20", out, src], capsys)
+    assert st == 0 and "Total number of unique k-mers: 94" in err, err
+    oracle_file(O.BYTE, 20, 1e3, 2, [ABUND], str(tmp_path / "o.ct"))
+    assert same_file(out, str(tmp_path / "o.ct"))
