@@ -116,6 +116,16 @@ int  kh_graph_clear(kh_graph *g);
  * Returns this call's share of (reads, k-mers).  mode 1 = consume_seqfile_and_tag
  * (src/oxli/hashgraph.cc:290-320). */
 int kh_consume_parser(kh_graph *g, kh_parser *p, int mode, uint32_t *reads, uint64_t *kmers);
+
+/* Hashtable::consume_seqfile_with_mask / _banding / _banding_with_mask
+ * (src/oxli/hashtable.cc:152-274; khmer/_oxli/graphs.pyx:241-280).  Counts a
+ * k-mer only if its hash lies in band `band` of `num_bands`
+ * (compute_band_interval, src/oxli/kmer_hash.cc:262-276) and, when `mask` is
+ * not NULL, mask's count c of the hash satisfies c >= threshold
+ * (consume_masked) or c <= threshold.  num_bands == 0 disables banding.
+ * *kmers = k-mers counted.  KH_EVALUE if band > num_bands or mask == g. */
+int kh_consume_parser_filtered(kh_graph *g, kh_parser *p, uint32_t num_bands, uint32_t band, kh_graph *mask,
+                               uint32_t threshold, int consume_masked, uint32_t *reads, uint64_t *kmers);
 /* Hashtable::consume_string over a batch of reads (src/oxli/hashtable.cc:280-294).
  * seqs = concatenated reads, offsets[nreads+1]; clean != 0 applies
  * _to_valid_dna first (consume_seqfile semantics), 0 hashes raw (consume()). */

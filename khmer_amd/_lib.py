@@ -65,6 +65,7 @@ SIGNATURES = {
     "kh_group_consume_packed_fixed_device": (i32, [P, ctypes.POINTER(P), u64, u64]),
     "kh_group_counters": (i32, [P, PU64, PU64]),
     "kh_consume_parser": (i32, [P, P, i32, PU32, PU64]),
+    "kh_consume_parser_filtered": (i32, [P, P, u32, u32, P, u32, i32, PU32, PU64]),
     "kh_consume_seqs": (i32, [P, ctypes.c_char_p, PU64, u64, i32, PU64]),
     "kh_consume_packed_device": (i32, [P, P, P, u64, u64]),
     "kh_consume_packed_fixed_device": (i32, [P, P, u64, u32]),

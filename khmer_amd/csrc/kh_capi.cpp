@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <fstream>
+#include <memory>
 #include <new>
 #include <string>
 
@@ -305,6 +306,58 @@ int kh_consume_parser(kh_graph *h, kh_parser *ph, int mode, uint32_t *reads, uin
                 throw;
             }
             consume_batch(g, b, mode, &consumed);
+        }
+        *reads = (uint32_t)nreads;
+        *kmers = consumed;
+    });
+}
+
+int kh_consume_parser_filtered(kh_graph *h, kh_parser *ph, uint32_t num_bands, uint32_t band, kh_graph *mh,
+                               uint32_t threshold, int consume_masked, uint32_t *reads, uint64_t *kmers) {
+    *reads = 0;
+    *kmers = 0;
+    return guard([&] {
+        CHECK_PTR(h);
+        CHECK_PTR(ph);
+        Graph *g = h->g;
+        BandMask f;
+        if (num_bands) {
+            // compute_band_interval: note the reference's check is band > num_bands,
+            // and band == num_bands wraps to an empty interval in u64 arithmetic
+            if (band > num_bands)
+                fail(KH_EVALUE, "'band' must be in the interval [0, 'num_bands'), " + std::to_string(band) +
+                                    " not in [0, " + std::to_string(num_bands) + ")");
+            const uint64_t bs = UINT64_MAX / num_bands;
+            f.num_bands = num_bands;
+            f.band_lo = bs * band;
+            f.band_hi = bs * (band + 1);
+        }
+        if (mh) {
+            if (mh->g == g) fail(KH_EVALUE, "a table cannot be its own mask");
+            if (mh->g->device != g->device) fail(KH_EVALUE, "mask table is on another device");
+            f.mask = mh->g;
+            f.threshold = threshold;
+            f.consume_masked = consume_masked;
+        }
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        std::unique_ptr<std::lock_guard<std::recursive_mutex>> mlk;
+        if (f.mask) mlk.reset(new std::lock_guard<std::recursive_mutex>(f.mask->mu));
+        KH_HIP(hipSetDevice(g->device));
+        HostBatch b;
+        b.hash = g->hash;
+        bool done = false;
+        uint64_t consumed = 0, nreads = 0;
+        while (!done) {
+            b.clear();
+            try {
+                parser_fill_batch(ph->p, b, g->k, g->batch_kmers, batch_bases_cap(g), &done, &nreads);
+            } catch (...) {
+                consumed += engine_consume_filtered(g, b, f);
+                *reads = (uint32_t)nreads;
+                *kmers = consumed;
+                throw;
+            }
+            consumed += engine_consume_filtered(g, b, f);
         }
         *reads = (uint32_t)nreads;
         *kmers = consumed;

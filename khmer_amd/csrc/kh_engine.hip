@@ -25,6 +25,7 @@
 #include <vector>
 
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
 
 #include "kh_apply.cuh"
 #include "kh_internal.h"
@@ -604,6 +605,61 @@ void engine_hash_batch(Graph *g, const HostBatch &b, uint64_t *h_out) {
     KH_HIP(hipMemcpyAsync(h_out, d, nk * 8, hipMemcpyDeviceToHost, g->stream));
     KH_HIP(hipStreamSynchronize(g->stream));
     KH_HIP(hipFree(d));
+}
+
+uint64_t engine_consume_filtered(Graph *g, const HostBatch &b, const BandMask &f) {
+    const uint64_t nk = b.nkmers(), nr = b.nreads();
+    if (!nk) return 0;
+    KmerFilter F{};
+    F.band = f.num_bands != 0;
+    F.band_lo = f.band_lo;
+    F.band_hi = f.band_hi;
+    if (f.mask) {
+        engine_sync_bigcounts(f.mask);
+        F.mask = 1;
+        F.MP = f.mask->prm;
+        F.mtab = f.mask->d_tab;
+        F.mbc_keys = f.mask->d_bc_keys;
+        F.mbc_vals = f.mask->d_bc_vals;
+        F.mbc_n = f.mask->d_bc_n;
+        F.threshold = f.threshold;
+        F.consume_masked = f.consume_masked;
+    }
+    upload_batch(g, b);
+    uint64_t *d_h = nullptr, *d_sel = nullptr, *d_n = nullptr;
+    uint8_t *d_keep = nullptr;
+    void *tmp = nullptr;
+    KH_HIP(hipMalloc((void **)&d_h, nk * 8));
+    KH_HIP(hipMalloc((void **)&d_sel, nk * 8));
+    KH_HIP(hipMalloc((void **)&d_keep, nk));
+    KH_HIP(hipMalloc((void **)&d_n, 8));
+    const uint64_t tiles = (nk + Q_TILE - 1) / Q_TILE;
+    const size_t lds = 16 + (Q_TILE + 2) * 8;
+    if (b.hash == MURMUR) {
+        SrcBytes s = src_bytes(g, g->ws.d_bytes);
+        s.koff = g->ws.d_koff;
+        s.nreads = nr;
+        hipLaunchKernelGGL(k_kmer_filter<SrcBytes>, dim3((unsigned)tiles), dim3(Q_THREADS), lds, g->stream, s, nk, F,
+                           d_h, d_keep);
+    } else {
+        SrcTwoBit s = src_twobit(g, g->ws.d_words);
+        s.koff = g->ws.d_koff;
+        s.nreads = nr;
+        hipLaunchKernelGGL(k_kmer_filter<SrcTwoBit>, dim3((unsigned)tiles), dim3(Q_THREADS), lds, g->stream, s, nk,
+                           F, d_h, d_keep);
+    }
+    KH_HIP(hipGetLastError());
+    size_t bytes = 0;
+    KH_HIP(rocprim::select(nullptr, bytes, d_h, d_keep, d_sel, d_n, (size_t)nk, g->stream));
+    KH_HIP(hipMalloc(&tmp, bytes));
+    KH_HIP(rocprim::select(tmp, bytes, d_h, d_keep, d_sel, d_n, (size_t)nk, g->stream));
+    uint64_t kept = 0;
+    KH_HIP(hipMemcpyAsync(&kept, d_n, 8, hipMemcpyDeviceToHost, g->stream));
+    KH_HIP(hipStreamSynchronize(g->stream));
+    if (kept) engine_consume_hashes(g, d_sel, kept, nullptr);
+    KH_HIP(hipStreamSynchronize(g->stream));
+    for (void *p : {(void *)d_h, (void *)d_sel, (void *)d_keep, (void *)d_n, tmp}) KH_HIP(hipFree(p));
+    return kept;
 }
 
 void engine_get_counts(Graph *g, const uint64_t *h_hashes, uint64_t n, uint16_t *out) {

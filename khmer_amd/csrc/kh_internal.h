@@ -192,6 +192,16 @@ void engine_consume_bytes(Graph *g, const uint8_t *d_bytes, const uint64_t *d_ko
 void engine_consume_hashes(Graph *g, const uint64_t *d_hashes, uint64_t n, const PassOut *out);
 void engine_consume_host(Graph *g, const HostBatch &b, const PassOut *out);
 void engine_get_counts(Graph *g, const uint64_t *h_hashes, uint64_t n, uint16_t *out);
+// consume_seqfile_banding / _with_mask (hashtable.cc:152-274): only k-mers in
+// the band and passing the mask are counted; returns how many were
+struct BandMask {
+    uint32_t num_bands = 0;          // 0: no banding
+    uint64_t band_lo = 0, band_hi = 0;
+    Graph *mask = nullptr;           // nullptr: no mask
+    uint32_t threshold = 0;
+    int consume_masked = 0;
+};
+uint64_t engine_consume_filtered(Graph *g, const HostBatch &b, const BandMask &f);
 void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, float *sd);
 void engine_sync_bigcounts(Graph *g);
 void engine_download_table(Graph *g, int i, uint8_t *dst);

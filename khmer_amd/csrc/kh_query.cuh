@@ -65,6 +65,46 @@ __global__ void __launch_bounds__(Q_THREADS) k_kmer_hashes(Src src, uint64_t nkm
     for (uint64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) out[j] = kmer_hash(src, s_koff, tr, j);
 }
 
+// Band / mask filter of the consume_seqfile_banding / _with_mask variants
+// (src/oxli/hashtable.cc:152-274): keep k-mer j iff its hash lies in
+// [band_lo, band_hi) (when banding) and the mask table's count c satisfies
+// c >= threshold (consume_masked) or c <= threshold (otherwise).  Writes the
+// hash and a keep flag per k-mer; order is preserved by the compaction after.
+struct KmerFilter {
+    int band;                 // banding on
+    uint64_t band_lo, band_hi;
+    int mask;                 // mask on
+    Params MP;                // mask table geometry
+    const uint8_t *mtab;
+    const uint64_t *mbc_keys;
+    const uint16_t *mbc_vals;
+    uint64_t mbc_n;
+    uint32_t threshold;
+    int consume_masked;
+};
+
+template <class Src>
+__global__ void __launch_bounds__(Q_THREADS) k_kmer_filter(Src src, uint64_t nkmers, KmerFilter F, uint64_t *out,
+                                                         uint8_t *keep) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *s_meta = (uint64_t *)smem;
+    uint64_t *s_koff = s_meta + 2;
+    const uint64_t j0 = (uint64_t)blockIdx.x * Q_TILE;
+    const uint64_t j1 = min(nkmers, j0 + Q_TILE);
+    TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
+    block_sync();
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
+        const uint64_t h = kmer_hash(src, s_koff, tr, j);
+        bool k = !F.band || (h >= F.band_lo && h < F.band_hi);
+        if (k && F.mask) {
+            const uint32_t c = get_count_dev(F.MP, F.mtab, h, F.mbc_keys, F.mbc_vals, F.mbc_n);
+            k = F.consume_masked ? c >= F.threshold : c <= F.threshold;
+        }
+        out[j] = h;
+        keep[j] = k ? 1 : 0;
+    }
+}
+
 // counts of every k-mer of a batch (for get_median_count)
 template <class Src>
 __global__ void __launch_bounds__(Q_THREADS) k_kmer_counts(Params P, Src src, uint64_t nkmers, const uint8_t *tab,

@@ -285,6 +285,50 @@ class Hashtable(object):
         """Count all k-mers from file_name (or a shared ReadParser)."""
         return self._consume_parser(parser_or_filename, 0)
 
+    def _consume_filtered(self, parser_or_filename, num_bands, band, mask, threshold, consume_masked):
+        if mask is not None and not isinstance(mask, Hashtable):
+            raise TypeError("mask must be a table")
+        if num_bands == 0 and mask is None:
+            return self.consume_seqfile(parser_or_filename)
+        if num_bands < 0 or band < 0:
+            raise OverflowError("can't convert negative value to unsigned int")
+        parser, owned = self._get_parser(parser_or_filename)
+        reads, kmers = ctypes.c_uint32(), ctypes.c_uint64()
+        try:
+            rc = lib.kh_consume_parser_filtered(
+                self._g, parser.handle, int(num_bands), int(band),
+                None if mask is None else mask._g, int(threshold) & 0xFFFFFFFF,
+                1 if consume_masked else 0, ctypes.byref(reads), ctypes.byref(kmers))
+            self._refresh_mirrors()
+            check(rc)
+        finally:
+            if owned is not None:
+                owned.close()
+        return reads.value, kmers.value
+
+    def consume_seqfile_with_mask(self, parser_or_filename, mask, threshold=0, consume_masked=False):
+        """Count the k-mers whose count in `mask` is <= threshold (or >= with
+        consume_masked) (graphs.pyx:241-252)."""
+        if not isinstance(mask, Hashtable):
+            raise TypeError("mask must be a table")
+        return self._consume_filtered(parser_or_filename, 0, 0, mask, threshold, consume_masked)
+
+    def consume_seqfile_banding(self, parser_or_filename, num_bands, band):
+        """Count the k-mers whose hash falls in band `band` of `num_bands`
+        (graphs.pyx:254-264)."""
+        if int(num_bands) == 0:
+            raise ValueError("num_bands must be > 0")
+        return self._consume_filtered(parser_or_filename, num_bands, band, None, 0, False)
+
+    def consume_seqfile_banding_with_mask(self, parser_or_filename, num_bands, band, mask, threshold=0,
+                                          consume_masked=False):
+        """Banding and mask together (graphs.pyx:266-280)."""
+        if int(num_bands) == 0:
+            raise ValueError("num_bands must be > 0")
+        if not isinstance(mask, Hashtable):
+            raise TypeError("mask must be a table")
+        return self._consume_filtered(parser_or_filename, num_bands, band, mask, threshold, consume_masked)
+
     def abundance_distribution(self, parser_or_filename, tracking):
         """Calculate the k-mer abundance distribution over input reads."""
         if not isinstance(tracking, Hashtable):

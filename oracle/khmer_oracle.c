@@ -673,6 +673,63 @@ int or_consume_fastx(or_table *t, const char *path, int mode, uint32_t *reads, u
     return rc == -3 ? -3 : (rc < 0 ? -2 : 0);
 }
 
+/* Hashtable::consume_seqfile_with_mask / _banding / _banding_with_mask:
+ * src/oxli/hashtable.cc:152-274; band interval: compute_band_interval
+ * src/oxli/kmer_hash.cc:262-276 (u64 wraparound kept).  num_bands == 0: no
+ * banding; mask == NULL: no mask.  Returns -4 for band > num_bands. */
+typedef struct {
+    or_table *t;
+    const or_table *mask;
+    int band;
+    uint64_t lo, hi;
+    uint32_t threshold;
+    int consume_masked;
+    uint64_t n;
+} filt_ctx;
+static void cb_filtered(void *ctx, uint64_t h) {
+    filt_ctx *f = ctx;
+    if (f->band && !(h >= f->lo && h < f->hi)) return;
+    if (f->mask) {
+        uint32_t c = (uint32_t)or_get(f->mask, h);
+        if (!(f->consume_masked ? c >= f->threshold : c <= f->threshold)) return;
+    }
+    or_add(f->t, h);
+    f->n++;
+}
+int or_consume_fastx_filtered(or_table *t, const char *path, uint32_t num_bands, uint32_t band,
+                              const or_table *mask, uint32_t threshold, int consume_masked,
+                              uint32_t *reads, uint64_t *kmers) {
+    *reads = 0; *kmers = 0;
+    filt_ctx f = { t, mask, num_bands != 0, 0, 0, threshold, consume_masked, 0 };
+    if (num_bands) {
+        if (band > num_bands) {
+            set_err("'band' must be in the interval [0, 'num_bands'), %u not in [0, %u)", band, num_bands);
+            return -4;
+        }
+        uint64_t bs = UINT64_MAX / num_bands;
+        f.lo = bs * band;
+        f.hi = bs * (uint64_t)(band + 1);
+    }
+    or_parser *p = or_parser_open(path);
+    if (!p) return -1;
+    const char *name, *seq, *qual;
+    size_t sl, ql;
+    char *clean = NULL;
+    size_t cap = 0;
+    int rc;
+    while ((rc = or_parser_next(p, &name, &seq, &qual, &sl, &ql)) == 1) {
+        if (sl + 1 > cap) { cap = (sl + 1) * 2; clean = realloc(clean, cap); }
+        for (size_t i = 0; i < sl; i++) clean[i] = clean_base((unsigned char)seq[i]);
+        clean[sl] = 0;
+        iterate_kmers(t, clean, sl, cb_filtered, &f);
+        (*reads)++;
+    }
+    *kmers = f.n;
+    free(clean);
+    or_parser_close(p);
+    return rc == -3 ? -3 : (rc < 0 ? -2 : 0);
+}
+
 uint64_t or_consume_batch(or_table *t, const char *seqs, const uint64_t *offs, uint64_t nreads) {
     uint64_t total = 0;
     char *clean = NULL;

@@ -68,6 +68,10 @@ uint64_t  or_kmer_hashes(const or_table *t, const char *s, size_t len, uint64_t 
  * 1 = consume_seqfile_and_tag.  Returns 0 ok, <0 error (message via or_last_error). */
 int       or_consume_fastx(or_table *t, const char *path, int mode,
                            uint32_t *reads, uint64_t *kmers);
+/* consume_seqfile_with_mask / _banding / _banding_with_mask (hashtable.cc:152-274) */
+int       or_consume_fastx_filtered(or_table *t, const char *path, uint32_t num_bands, uint32_t band,
+                                    const or_table *mask, uint32_t threshold, int consume_masked,
+                                    uint32_t *reads, uint64_t *kmers);
 /* consume an in-memory batch: seqs concatenated, offs[nreads+1]; cleaned per read */
 uint64_t  or_consume_batch(or_table *t, const char *seqs, const uint64_t *offs, uint64_t nreads);
 

@@ -55,6 +55,8 @@ def lib():
             "or_consume_string": (u32, [P, ctypes.c_char_p, ctypes.c_size_t]),
             "or_kmer_hashes": (u64, [P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(u64)]),
             "or_consume_fastx": (i32, [P, ctypes.c_char_p, i32, ctypes.POINTER(u32), ctypes.POINTER(u64)]),
+            "or_consume_fastx_filtered": (i32, [P, ctypes.c_char_p, u32, u32, P, u32, i32,
+                                                ctypes.POINTER(u32), ctypes.POINTER(u64)]),
             "or_consume_batch": (u64, [P, ctypes.c_char_p, ctypes.POINTER(u64), u64]),
             "or_consume_batch_mt": (u64, [P, ctypes.c_char_p, ctypes.POINTER(u64), u64, i32]),
             "or_median": (i32, [P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint16),
@@ -178,6 +180,17 @@ class Table:
         r, k = ctypes.c_uint32(), ctypes.c_uint64()
         rc = lib().or_consume_fastx(self._h, _b(path), 1 if tag else 0,
                                     ctypes.byref(r), ctypes.byref(k))
+        if rc in (-1, -3):
+            raise OSError(err())
+        if rc < 0:
+            raise ValueError(err())
+        return r.value, k.value
+
+    def consume_fastx_filtered(self, path, num_bands=0, band=0, mask=None, threshold=0, consume_masked=False):
+        r, k = ctypes.c_uint32(), ctypes.c_uint64()
+        rc = lib().or_consume_fastx_filtered(self._h, _b(path), num_bands, band,
+                                             None if mask is None else mask._h, threshold & 0xFFFFFFFF,
+                                             1 if consume_masked else 0, ctypes.byref(r), ctypes.byref(k))
         if rc in (-1, -3):
             raise OSError(err())
         if rc < 0:

@@ -393,3 +393,87 @@ def test_normc20k20_layout():
         assert val > 255
         # a bigcount only exists where every table's bin is saturated
         assert all(t[key % p] == 255 for t, p in zip(tables, sizes))
+
+
+# --- banding / mask consume: tests/test_banding.py, tests/test_counttable.py:83-187 ---
+def _get(o, kmer):
+    return o.get(o.hash(kmer))
+
+
+@pytest.mark.parametrize("kind", [O.BIT, O.BYTE])
+def test_oracle_banding_kat(kind):
+    """tests/test_banding.py:140-157 (Nodetable / Counttable, k=31, 1e5 x 4)."""
+    o = O.Table(kind, 31, primes(4, 100000), hash=O.MURMUR)
+    assert o.consume_fastx_filtered(data("bogus.fa"), 8, 3) == (1, 3)
+    for kmer, want in [("CGGCTATTATCTGAGCTCAAGACTAATACGC", 1), ("TATTATCTGAGCTCAAGACTAATACGCGCTG", 1),
+                       ("TGAGCTCAAGACTAATACGCGCTGGCCACTG", 1), ("GTACGGCTATTATCTGAGCTCAAGACTAATA", 0),
+                       ("TTATCTGAGCTCAAGACTAATACGCGCTGGC", 0), ("GCTCAAGACTAATACGCGCTGGCCACTGGTA", 0)]:
+        assert _get(o, kmer) == want, kmer
+
+
+def test_oracle_banding_bad_band():
+    """tests/test_banding.py:120-136."""
+    o = O.Table(O.BYTE, 31, primes(4, 100000), hash=O.MURMUR)
+    with pytest.raises(ValueError, match="'band' must be in the interval"):
+        o.consume_fastx_filtered(data("bogus.fa"), 8, 13)
+    with pytest.raises(OSError):
+        o.consume_fastx_filtered("file-no-exist.fa", 16, 3)
+
+
+@pytest.mark.parametrize("numbands", [3, 11, 23, 29])
+def test_oracle_banding_to_disk(tmp_path, numbands):
+    """tests/test_banding.py:85-117: all bands consumed in turn give the same
+    saved table bytes as one plain consume (Counttable k=21, 5e6/4 x 4)."""
+    a = O.Table(O.BYTE, 21, primes(4, 5e6 / 4), hash=O.MURMUR)
+    a.consume_fastx(data("banding-reads.fq.gz"))
+    b = O.Table(O.BYTE, 21, primes(4, 5e6 / 4), hash=O.MURMUR)
+    total = 0
+    for band in range(numbands):
+        total += b.consume_fastx_filtered(data("banding-reads.fq.gz"), numbands, band)[1]
+    a.save(str(tmp_path / "a.ct"))
+    b.save(str(tmp_path / "b.ct"))
+    assert open(str(tmp_path / "a.ct"), "rb").read() == open(str(tmp_path / "b.ct"), "rb").read()
+
+
+def _mask_from(path):
+    m = O.Table(O.BYTE, 13, primes(4, 1e3), hash=O.MURMUR)
+    m.consume_fastx(path)
+    return m
+
+
+def test_oracle_consume_with_mask():
+    """tests/test_counttable.py:83-110."""
+    mask = _mask_from(data("seq-a.fa"))
+    o = O.Table(O.BYTE, 13, primes(4, 1e3), hash=O.MURMUR)
+    assert o.consume_fastx_filtered(data("seq-b.fa"), mask=mask) == (1, 3)
+    assert [_get(o, k) for k in ["GATTTGAGAAAAA", "ATTTGAGAAAAAA", "TTTGAGAAAAAAG", "TTGAGAAAAAAGT"]] == [0, 1, 1, 1]
+
+
+def test_oracle_consume_banding_with_mask():
+    """tests/test_counttable.py:113-136."""
+    mask = _mask_from(data("seq-a.fa"))
+    o = O.Table(O.BYTE, 13, primes(4, 1e3), hash=O.MURMUR)
+    assert o.consume_fastx_filtered(data("seq-b.fa"), 4, 1, mask=mask) == (1, 1)
+    assert [_get(o, k) for k in ["GATTTGAGAAAAA", "ATTTGAGAAAAAA", "TTTGAGAAAAAAG", "TTGAGAAAAAAGT"]] == [0, 0, 0, 1]
+
+
+def test_oracle_consume_with_mask_threshold():
+    """tests/test_counttable.py:139-173."""
+    mask = O.Table(O.BYTE, 13, primes(4, 1e3), hash=O.MURMUR)
+    for _ in range(3):
+        mask.consume("TAGATCTGCTTGAAACAAGTGGATTTGAGAAAAA")
+    for _ in range(2):
+        mask.consume("TAGATCTGCTTGAAACAAGTGGATTTGAGAAAAAAGT")
+    o = O.Table(O.BYTE, 13, primes(4, 1e3), hash=O.MURMUR)
+    assert o.consume_fastx_filtered(data("seq-b.fa"), mask=mask, threshold=3) == (1, 3)
+    assert [_get(o, k) for k in ["GATTTGAGAAAAA", "ATTTGAGAAAAAA", "TTTGAGAAAAAAG", "TTGAGAAAAAAGT"]] == [0, 1, 1, 1]
+
+
+def test_oracle_consume_with_mask_complement():
+    """tests/test_counttable.py:176-187."""
+    mask = O.Table(O.BIT, 13, primes(4, 1e3), hash=O.MURMUR)
+    mask.consume("TGCTTGAAACAAGTG")
+    o = O.Table(O.BYTE, 13, primes(4, 1e3), hash=O.MURMUR)
+    o.consume_fastx_filtered(data("seq-b.fa"), mask=mask, threshold=1, consume_masked=True)
+    assert [_get(o, k) for k in ["TGCTTGAAACAAG", "GCTTGAAACAAGT", "CTTGAAACAAGTG"]] == [1, 1, 1]
+    assert [_get(o, k) for k in ["GAAACAAGTGGAT", "AAACAAGTGGATT", "AACAAGTGGATTT"]] == [0, 0, 0]
