@@ -34,6 +34,18 @@ def algorithmic_bytes_per_kmer(L, k, n_tables):
     return (L / 4.0) / (L - k + 1) + 2.0 * n_tables
 
 
+# SURVEY.md §8(d) configurations: graph class, k, per-table size.  C2 is the
+# BASELINE.json headline (the default); C3 / C5 measure the bit and nibble
+# storages on the same pipeline (C5 as its 2-bit SmallCountgraph variant, k=31).
+CONFIGS = {
+    "C2": ("Countgraph", 21, 1e9),
+    "C3": ("Nodegraph", 31, 4e9),
+    "C5": ("SmallCountgraph", 31, 8e9),
+}
+DTYPE = {"Countgraph": "u8", "Nodegraph": "u1 (bit)", "SmallCountgraph": "u4 (nibble)"}
+ORACLE_KIND = {"Countgraph": "BYTE", "Nodegraph": "BIT", "SmallCountgraph": "NIBBLE"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -41,9 +53,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reads", type=int, default=50_000_000, help="reads per GPU")
     ap.add_argument("--read-len", type=int, default=150)
-    ap.add_argument("-k", type=int, default=21)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="C2",
+                    help="graph class / k / table size preset (SURVEY.md §8(d))")
+    ap.add_argument("-k", type=int, default=None, help="override the preset's k")
     ap.add_argument("--tables", type=int, default=4)
-    ap.add_argument("-x", type=float, default=1e9)
+    ap.add_argument("-x", type=float, default=None, help="override the preset's table size")
     ap.add_argument("--batch-kmers", type=int, default=1 << 30)
     ap.add_argument("--no-bigcount", action="store_true")
     ap.add_argument("--ablate", type=int, default=0,
@@ -53,7 +67,12 @@ def parse():
     ap.add_argument("--cpu-reads", type=int, default=1_000_000,
                     help="reads in the oracle CPU-baseline sample (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.graph, k, x = CONFIGS[a.config]
+    a.k = k if a.k is None else a.k
+    a.x = x if a.x is None else a.x
+    a.bigcount = a.graph == "Countgraph" and not a.no_bigcount
+    return a
 
 
 def kernel_stats(lib, g):
@@ -72,8 +91,8 @@ def cpu_baseline(args, sizes):
     synthetic stream into the same-size tables."""
     from oracle import oracle as O
     from khmer_amd import synth
-    t = O.Table(O.BYTE, args.k, sizes)
-    t.set_use_bigcount(not args.no_bigcount)
+    t = O.Table(getattr(O, ORACLE_KIND[args.graph]), args.k, sizes)
+    t.set_use_bigcount(args.bigcount)
     total, secs = 0, 0.0
     chunk = 100_000
     for r0 in range(0, args.cpu_reads, chunk):
@@ -88,8 +107,8 @@ def cpu_baseline(args, sizes):
         "cores": 1,
         "kind": "port",
         "sample": "%d synthetic %d bp reads (%d k-mers, the first reads of the benchmark stream) "
-                  "into the same 4x%.0e Countgraph, oracle/khmer_oracle.c single thread"
-                  % (args.cpu_reads, args.read_len, total, args.x),
+                  "into the same %dx%.0e %s, oracle/khmer_oracle.c single thread"
+                  % (args.cpu_reads, args.read_len, total, args.tables, args.x, args.graph),
     }
 
 
@@ -175,7 +194,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "k-mers hashed/sec into Countgraph (k=21, 4x1e9)",
+            "metric": "k-mers hashed/sec into %s (k=%d, %dx%.0e)" % (args.graph, k, nt, args.x),
             "value": value,
             "unit": "k-mers/s",
             "n_gpus": world,
@@ -185,12 +204,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8",
+            "dtype": DTYPE[args.graph],
             "data": "synthetic (seeded SplitMix64 reads generated in HBM)",
             "config": {
                 "workload": runner.config_name(),
                 "k": k, "n_tables": nt, "table_sizes": sizes, "reads_per_gpu": nreads,
-                "read_len": L, "kmers_per_gpu_per_step": nkmers, "bigcount": not args.no_bigcount,
+                "read_len": L, "kmers_per_gpu_per_step": nkmers, "bigcount": args.bigcount,
                 "batch_kmers": args.batch_kmers,
                 "parallelism": ("shard%d" % world) if world > 1 else "single",
             },
@@ -208,8 +227,8 @@ class SingleGpuBench(object):
 
     def config_name(self):
         a = self.args
-        return "Countgraph k=%d %dx%.0e, %d x %d bp synthetic reads, 1xMI355X" % (
-            a.k, a.tables, a.x, a.reads, a.read_len)
+        return "%s k=%d %dx%.0e, %d x %d bp synthetic reads, 1xMI355X" % (
+            a.graph, a.k, a.tables, a.x, a.reads, a.read_len)
 
     def setup(self):
         import khmer_amd
@@ -217,8 +236,8 @@ class SingleGpuBench(object):
         from khmer_amd._lib import lib, check
         a = self.args
         self.lib, self._ck = lib, check
-        self.g = khmer_amd.Countgraph(a.k, a.x, a.tables)
-        if not a.no_bigcount:
+        self.g = getattr(khmer_amd, a.graph)(a.k, a.x, a.tables)
+        if a.bigcount:
             self.g.set_use_bigcount(True)
         check(lib.kh_graph_set_batch_kmers(self.g._g, a.batch_kmers))
         self.nkmers = a.reads * (a.read_len - a.k + 1)

@@ -184,7 +184,7 @@ class ShardedCountgraphBench(object):
 
     def config_name(self):
         a = self.args
-        return "Countgraph k=%d %dx%.0e sharded over %dxMI355X, %d x %d bp synthetic reads per GPU" % (
+        return a.graph + " k=%d %dx%.0e sharded over %dxMI355X, %d x %d bp synthetic reads per GPU" % (
             a.k, a.tables, a.x, self.world, a.reads, a.read_len)
 
     def setup(self):
@@ -196,8 +196,9 @@ class ShardedCountgraphBench(object):
         self.dist = dist
         obj = [ShardedGraph.unique_id() if self.rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        self.g = ShardedGraph("Countgraph", a.k, self.sizes, self.world, self.rank, self.device, uid=obj[0])
-        self.g.set_use_bigcount(not a.no_bigcount)
+        self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device, uid=obj[0])
+        if a.bigcount:
+            self.g.set_use_bigcount(True)
         self.g.set_batch_kmers(a.batch_kmers)
         nwords = a.reads * a.read_len // 32 + 2
         self.words, self.koff = ctypes.c_void_p(), ctypes.c_void_p()
