@@ -245,6 +245,19 @@ void engine_collect_events(Graph *g) {
 }
 #define TIMED(name, ...) do { KTimer kt_(g, name); __VA_ARGS__; } while (0)
 
+// level-1 scatter instance for a tail mode and k-mers per thread (8 / nt)
+template <class Src>
+using L1Fn = void (*)(Params, Src, uint64_t, uint32_t, uint32_t, int, int, uint64_t *, uint64_t *);
+template <class Src>
+static L1Fn<Src> l1_kernel(bool seg, int kpt) {
+    switch (kpt) {
+        case 8: return seg ? k_scatter_l1<Src, 8, 8> : k_scatter_l1<Src, 0, 8>;
+        case 4: return seg ? k_scatter_l1<Src, 8, 4> : k_scatter_l1<Src, 0, 4>;
+        case 2: return seg ? k_scatter_l1<Src, 8, 2> : k_scatter_l1<Src, 0, 2>;
+        default: return seg ? k_scatter_l1<Src, 8, 1> : k_scatter_l1<Src, 0, 1>;
+    }
+}
+
 // LDS footprints
 static size_t lds_window(bool window, int tile_kmers) { return 16 + (window ? (size_t)(tile_kmers + 2) * 8 : 0); }
 static size_t lds_hist_l1(const Params &P, bool window) {
@@ -322,9 +335,9 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
         const int nt = std::min(L1_MAX_RPT, P.n - t0);
         const int kpt = std::max(1, L1_MAX_RPT / nt);
         const int tile_kmers = L1_THREADS * kpt;
-        auto kfn = l1_seg(P) ? k_scatter_l1<Src, 8> : k_scatter_l1<Src, 0>;
-        TIMED("scatter_l1", hipLaunchKernelGGL(kfn, dim3(q.nch1), dim3(L1_THREADS), lds_scatter_l1(P, window, tile_kmers),
-                                               st, P, src, nkmers, q.ck1, q.nch1, kpt, t0, nt, w.moff, w.rec1));
+        TIMED("scatter_l1", hipLaunchKernelGGL(l1_kernel<Src>(l1_seg(P) != 0, kpt), dim3(q.nch1), dim3(L1_THREADS),
+                                               lds_scatter_l1(P, window, tile_kmers), st, P, src, nkmers, q.ck1,
+                                               q.nch1, t0, nt, w.moff, w.rec1));
     }
     if (check_mode()) check_holes(g, w.rec1, q.recs, "scatter_l1");
     // level 2
@@ -785,12 +798,12 @@ static void set_lds_limits() {
     (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_bit, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
 #define KH_LDS_MAX(...) (void)hipFuncSetAttribute((const void *)__VA_ARGS__, hipFuncAttributeMaxDynamicSharedMemorySize, lim)
-    KH_LDS_MAX(k_scatter_l1<SrcTwoBit, 0>);
-    KH_LDS_MAX(k_scatter_l1<SrcTwoBit, 8>);
-    KH_LDS_MAX(k_scatter_l1<SrcBytes, 0>);
-    KH_LDS_MAX(k_scatter_l1<SrcBytes, 8>);
-    KH_LDS_MAX(k_scatter_l1<SrcHashes, 0>);
-    KH_LDS_MAX(k_scatter_l1<SrcHashes, 8>);
+    for (int kpt : {1, 2, 4, 8})
+        for (bool seg : {false, true}) {
+            KH_LDS_MAX(l1_kernel<SrcTwoBit>(seg, kpt));
+            KH_LDS_MAX(l1_kernel<SrcBytes>(seg, kpt));
+            KH_LDS_MAX(l1_kernel<SrcHashes>(seg, kpt));
+        }
     KH_LDS_MAX((k_scatter_l2<PT_THREADS, L2_SEG>));
     KH_LDS_MAX((k_scatter_w<PT_THREADS, 8>));
 #undef KH_LDS_MAX

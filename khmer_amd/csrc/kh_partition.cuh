@@ -139,6 +139,8 @@ struct Emit {
     T *tail;           // [F*SEG]
     uint32_t *hist;    // [F] this tile's count
     uint32_t *lstart;  // [F] this tile's LDS start
+    uint64_t *dl;      // [F] output position minus LDS position (prepare())
+    uint64_t *lim;     // [F] first output position that goes to the tail (prepare())
 
     __device__ __forceinline__ void init(uint32_t d, uint64_t pos) const {
         lcur[d] = pos;
@@ -160,10 +162,25 @@ struct Emit {
             if (sl >= hskip[d] && a + sl < lc) out[a + sl] = tail[x];
         }
     }
-    // phase 2 (after a barrier): staged record q of destination d
-    __device__ __forceinline__ void put(uint32_t d, uint32_t q, T v, bool last, T *out) const {
+    // after the tile scan: per-destination placement constants for put()
+    __device__ __forceinline__ void prepare(uint32_t F, bool last) const {
+        for (uint32_t d = threadIdx.x; d < F; d += blockDim.x) {
+            const uint64_t lc = lcur[d];
+            dl[d] = lc - lstart[d];
+            lim[d] = TAILS ? flush_end(lc + hist[d], last) : ~0ull;
+        }
+    }
+    // phase 2 (after a barrier): staged record q of destination d, from the
+    // cursors directly (no prepare())
+    __device__ __forceinline__ void put_cur(uint32_t d, uint32_t q, T v, bool last, T *out) const {
         const uint64_t pos = lcur[d] + (q - lstart[d]);
         if (!TAILS || pos < flush_end(lcur[d] + hist[d], last)) out[pos] = v;
+        else tail[d * SEG + (uint32_t)(pos & (SEG - 1))] = v;
+    }
+    // the same with the prepare()d constants
+    __device__ __forceinline__ void put(uint32_t d, uint32_t q, T v, T *out) const {
+        const uint64_t pos = dl[d] + q;
+        if (!TAILS || pos < lim[d]) out[pos] = v;
         else tail[d * SEG + (uint32_t)(pos & (SEG - 1))] = v;
     }
     // register-direct form: record of destination d with tile rank r
@@ -239,12 +256,13 @@ __global__ void __launch_bounds__(1024) k_plan_l2(uint32_t F1, uint32_t nch1, co
     if (threadIdx.x == 0) ch2[F1] = (uint32_t)chunks;
 }
 
-// level-1 scatter of tables [t0, t0+nt) (nt <= 8), one workgroup per chunk;
-// records stay in registers between the tile histogram and the placement.
-// The chunk's cursors are written back so a following table group continues.
-template <class Src, int SEG>
+// level-1 scatter of tables [t0, t0+nt) (nt <= 8), KPT = 8 / nt k-mers per
+// thread per tile, one workgroup per chunk; records stay in registers between
+// the tile histogram and the placement.  The chunk's cursors are written back
+// so a following table group continues.
+template <class Src, int SEG, int KPT>
 __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, uint64_t nkmers, uint32_t ck1,
-                                                          uint32_t nch1, int kpt, int t0, int nt, uint64_t *O1,
+                                                          uint32_t nch1, int t0, int nt, uint64_t *O1,
                                                           uint64_t *rec) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t F1 = P.F1;
@@ -259,10 +277,10 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
     uint8_t *hskip = (uint8_t *)(s_wtot + 16);        // [F1]
     uint64_t *s_meta = (uint64_t *)(hskip + ((F1a + 7) & ~7u));
     uint64_t *s_koff = s_meta + 2;
-    const Emit<uint64_t, SEG> em{lcur, hskip, tail, hist, lstart};
+    const Emit<uint64_t, SEG> em{lcur, hskip, tail, hist, lstart, nullptr, nullptr};
     const int shift = P.s0 + P.s2;
     const uint64_t omask = (1ull << shift) - 1;
-    const int tile_kmers = L1_THREADS * kpt;
+    constexpr int TILE_KMERS = L1_THREADS * KPT;
 
     for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) em.init(b, O1[(uint64_t)b * nch1 + blockIdx.x]);
     const uint64_t c0 = (uint64_t)blockIdx.x * ck1;
@@ -274,23 +292,23 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
 #else
 #define PH(i) do { } while (0)
 #endif
-    // without a read-offset window the next tile's hashes are computed
-    // before this tile's stores are issued (loads and stores share one
-    // completion counter, so loads issued after the stores would wait for them)
+    // Without a read-offset window the next tile's input words are loaded a
+    // whole tile ahead (fetch) and hashed at the top of the tile (finish):
+    // the loads are issued before this tile's stores (loads and stores share
+    // one completion counter) and their latency hides behind the tile's work.
     const bool pre = !needs_window(src);
-    uint64_t hh[L1_MAX_RPT];
+    typename Src::Pend pend[KPT];
     if (pre) {
-        const TileReads tr0{0, 0};
 #pragma unroll
-        for (int a = 0; a < L1_MAX_RPT; a++) {
+        for (int a = 0; a < KPT; a++) {
             const uint64_t j = c0 + (uint64_t)a * L1_THREADS + threadIdx.x;
-            hh[a] = (a < kpt && j < min(c1, c0 + tile_kmers)) ? kmer_hash(src, s_koff, tr0, j) : 0;
+            if (j < min(c1, c0 + TILE_KMERS)) pend[a] = kmer_fetch(src, j);
         }
     }
-    const uint32_t ntiles = uniform_u32((uint32_t)((c1 - c0 + tile_kmers - 1) / tile_kmers));
+    const uint32_t ntiles = uniform_u32((uint32_t)((c1 - c0 + TILE_KMERS - 1) / TILE_KMERS));
     for (uint32_t ti = 0; ti < ntiles; ti++) {
-        const uint64_t j0 = c0 + (uint64_t)ti * tile_kmers;
-        const uint64_t j1 = min(c1, j0 + tile_kmers);
+        const uint64_t j0 = c0 + (uint64_t)ti * TILE_KMERS;
+        const uint64_t j1 = min(c1, j0 + TILE_KMERS);
         const bool last = ti + 1 == ntiles;
         block_sync();
         PH(0);
@@ -301,18 +319,17 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
         int nr = 0;
 #pragma unroll
         for (int q = 0; q < L1_MAX_RPT; q++) { G[q] = ~0ull; rank[q] = 0; jj[q] = 0; }
-        // pass A: hashes (all input loads in flight), bins, tile histogram (ranks)
-        if (!pre) {
+        // pass A: hashes, bins, tile histogram (ranks)
+        uint64_t hh[KPT];
 #pragma unroll
-            for (int a = 0; a < L1_MAX_RPT; a++) {
-                const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
-                hh[a] = (a < kpt && j < j1) ? kmer_hash(src, s_koff, tr, j) : 0;
-            }
+        for (int a = 0; a < KPT; a++) {
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            hh[a] = j < j1 ? (pre ? src.finish(pend[a]) : kmer_hash(src, s_koff, tr, j)) : 0;
         }
 #pragma unroll
-        for (int a = 0; a < L1_MAX_RPT; a++) {
+        for (int a = 0; a < KPT; a++) {
             const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
-            const bool ok = a < kpt && j < j1;
+            const bool ok = j < j1;
 #pragma unroll
             for (int q = 0; q < L1_MAX_RPT; q++) {
                 const int i = q - a * nt;  // table slot of register q for k-mer a
@@ -331,7 +348,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
         }
         block_sync();
         PH(1);
-        wave_exclusive_scan(hist, lstart, F1);
+        block_scan_hist(hist, lstart, F1, s_wtot);
         block_sync();
         PH(2);
         // pass B: place in LDS in bucket order
@@ -345,12 +362,11 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
             }
         }
         if (pre) {
-            const TileReads tr0{0, 0};
-            const uint64_t n0 = j0 + tile_kmers, n1 = min(c1, n0 + tile_kmers);
+            const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
 #pragma unroll
-            for (int a = 0; a < L1_MAX_RPT; a++) {
+            for (int a = 0; a < KPT; a++) {
                 const uint64_t j = n0 + (uint64_t)a * L1_THREADS + threadIdx.x;
-                hh[a] = (a < kpt && j < n1) ? kmer_hash(src, s_koff, tr0, j) : 0;
+                if (j < n1) pend[a] = kmer_fetch(src, j);
             }
         }
         em.flush_tails(F1, last, rec);
@@ -361,7 +377,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
 #pragma unroll
         for (int u = 0; u < L1_MAX_RPT; u++) {
             const uint32_t q = threadIdx.x + (uint32_t)u * L1_THREADS;
-            if (q < nrec) em.put(sb[q], q, stage[q], last, rec);
+            if (q < nrec) em.put_cur(sb[q], q, stage[q], last, rec);
         }
         block_sync();
         PH(4);
@@ -447,7 +463,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2(uint32_t F1, int s0, int
     uint64_t *tail = lcur + F2;                    // [F2*SEG]
     uint32_t *hist = (uint32_t *)(tail + F2 * SEG);  // [F2]
     uint8_t *hskip = (uint8_t *)(hist + F2);       // [F2]
-    const Emit<uint64_t, SEG> em{lcur, hskip, tail, hist, nullptr};
+    const Emit<uint64_t, SEG> em{lcur, hskip, tail, hist, nullptr, nullptr, nullptr};
     const uint64_t rmask = (1ull << s0) - 1;
     L2Chunk k;
     if (!l2_chunk(F1, off1, ch2, &k)) return;

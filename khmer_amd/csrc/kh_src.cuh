@@ -35,11 +35,26 @@ struct SrcCommon {
     int k;
 };
 
+// Every source also splits a hash into fetch() (issue the global loads) and
+// finish() (compute from the loaded registers), so a kernel can fetch the next
+// tile's k-mers a whole tile ahead of using them.
 struct SrcTwoBit : SrcCommon {
     const uint64_t *words;
     static constexpr bool kReads = true;
     __device__ __forceinline__ uint64_t at(uint64_t ja, uint64_t r) const {
         return canonical2(window2(words, ja + r * (uint64_t)(k - 1), k), k);
+    }
+    struct Pend {
+        uint64_t w0, w1;
+        uint32_t sh;
+    };
+    __device__ __forceinline__ Pend fetch(uint64_t ja, uint64_t r) const {
+        const uint64_t b = (ja + r * (uint64_t)(k - 1)) * 2;
+        return Pend{words[b >> 6], words[(b >> 6) + 1], (uint32_t)(b & 63)};
+    }
+    __device__ __forceinline__ uint64_t finish(const Pend &p) const {
+        const uint64_t x = p.sh ? ((p.w0 << p.sh) | (p.w1 >> (64 - p.sh))) : p.w0;
+        return canonical2(x >> (64 - 2 * k), k);
     }
 };
 
@@ -49,12 +64,18 @@ struct SrcBytes : SrcCommon {
     __device__ __forceinline__ uint64_t at(uint64_t ja, uint64_t r) const {
         return murmur_canonical(bytes + ja + r * (uint64_t)(k - 1), k);
     }
+    using Pend = uint64_t;   // Murmur reads k bytes: hashed at fetch time
+    __device__ __forceinline__ Pend fetch(uint64_t ja, uint64_t r) const { return at(ja, r); }
+    __device__ __forceinline__ uint64_t finish(Pend p) const { return p; }
 };
 
 struct SrcHashes : SrcCommon {
     const uint64_t *h;
     static constexpr bool kReads = false;
     __device__ __forceinline__ uint64_t at(uint64_t ja, uint64_t) const { return h[ja - kbase]; }
+    using Pend = uint64_t;
+    __device__ __forceinline__ Pend fetch(uint64_t ja, uint64_t) const { return h[ja - kbase]; }
+    __device__ __forceinline__ uint64_t finish(Pend p) const { return p; }
 };
 
 // LDS window of read offsets covering k-mer tile [j0, j1) (variable mode)
@@ -117,6 +138,15 @@ __device__ __forceinline__ uint64_t kmer_hash(const Src &src, const uint64_t *s_
         }
         return src.at(ja, r);
     }
+}
+
+// fetch half of kmer_hash for sources without a read window (fixed-length
+// reads or explicit hashes)
+template <class Src>
+__device__ __forceinline__ typename Src::Pend kmer_fetch(const Src &src, uint64_t j) {
+    const uint64_t ja = j + src.kbase;
+    if constexpr (!Src::kReads) return src.fetch(ja, 0);
+    else return src.fetch(ja, div_barrett(ja, src.kpr, src.kpr_m));
 }
 
 // hash of batch k-mer j without a tile window (rare paths: bigcount, outputs)
