@@ -174,8 +174,9 @@ def main():
         try:
             with open(args.traffic_json) as fh:
                 tj = json.load(fh)
-            if tj.get("kernel") == name and tj.get("config") == runner.config_name():
-                traffic = tj.get("hbm_bytes_per_launch")
+            if tj.get("config") == runner.config_name():
+                traffic = (tj["kernels"].get(name) if "kernels" in tj
+                           else tj.get("hbm_bytes_per_launch") if tj.get("kernel") == name else None)
         except (OSError, ValueError):
             pass
         step_s = elapsed / args.steps

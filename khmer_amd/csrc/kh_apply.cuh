@@ -502,7 +502,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_w(Params P, ApplyArgs A, in
     uint32_t *lstart = hist + FJa;                 // [FJ]
     uint32_t *s_wtot = lstart + FJa;               // [16]
     uint8_t *hskip = (uint8_t *)(s_wtot + 16);     // [FJ]
-    const Emit<uint32_t, SEG> em{lcur, hskip, tail, hist, lstart, nullptr, nullptr};
+    const Emit<uint32_t, SEG> em{lcur, hskip, tail, hist, lstart, nullptr, nullptr, nullptr, nullptr};
     for (uint32_t b = threadIdx.x; b < FJ; b += THREADS) em.init(b, O3[(uint64_t)b * nchw + blockIdx.x]);
     const uint32_t n = w_chunk_setup(P, A, A.rprefix[P.n], s_pre, s_e0);
     const uint32_t ntiles = uniform_u32((n + TILE - 1) / TILE);

@@ -271,9 +271,10 @@ static size_t lds_scatter_l1(const Params &P, bool window, int tile_kmers) {
            (size_t)L1_TILE_RECS * 2 + 64 + ((F1a + 7) & ~7u) + lds_window(window, tile_kmers);
 }
 constexpr int L2_SEG = 16;   // 128-B level-2 write segments
+constexpr int L2_RPT = 8;    // level-2 records per thread per tile
 static size_t lds_scatter_l2(const Params &P) {
     const size_t F2 = (size_t)1 << P.s2;
-    return F2 * 8 + F2 * 8 * L2_SEG + F2 * 4 + F2;
+    return F2 * 8 + F2 * 8 * L2_SEG + F2 * 4 + 8 + ((F2 + 1) & ~(size_t)1) * 2 + F2;
 }
 static size_t lds_scatter_w(uint32_t FJ) {
     const size_t FJa = (FJ + 3) & ~3u;
@@ -347,7 +348,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     TIMED("scan", scan_counts(g, w.mcnt, w.moff, F2 * q.nch2max));
     TIMED("off2", hipLaunchKernelGGL(k_off2, dim3((unsigned)std::min<uint64_t>((F1 * F2 + 255) / 256, 8192)),
                                      dim3(256), 0, st, (uint32_t)F1, P.s2, w.off1, w.ch2, w.moff, w.off2));
-    TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2<PT_THREADS, L2_SEG>), dim3(g2), dim3(PT_THREADS),
+    TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2<PT_THREADS, L2_SEG, L2_RPT>), dim3(g2), dim3(PT_THREADS),
                                            lds_scatter_l2(P), st, (uint32_t)F1, P.s0, P.s2, w.off1, w.ch2, w.moff,
                                            w.rec1, w.rec2));
 
@@ -804,7 +805,7 @@ static void set_lds_limits() {
             KH_LDS_MAX(l1_kernel<SrcBytes>(seg, kpt));
             KH_LDS_MAX(l1_kernel<SrcHashes>(seg, kpt));
         }
-    KH_LDS_MAX((k_scatter_l2<PT_THREADS, L2_SEG>));
+    KH_LDS_MAX((k_scatter_l2<PT_THREADS, L2_SEG, L2_RPT>));
     KH_LDS_MAX((k_scatter_w<PT_THREADS, 8>));
 #undef KH_LDS_MAX
     (void)hipFuncSetAttribute((const void *)k_mark, hipFuncAttributeMaxDynamicSharedMemorySize, lim);

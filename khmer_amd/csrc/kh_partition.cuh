@@ -141,6 +141,8 @@ struct Emit {
     uint32_t *lstart;  // [F] this tile's LDS start
     uint64_t *dl;      // [F] output position minus LDS position (prepare())
     uint64_t *lim;     // [F] first output position that goes to the tail (prepare())
+    uint16_t *flist;   // [F] destinations whose tail segment completes in this tile (note())
+    uint32_t *nflush;  // [1] entries in flist
 
     __device__ __forceinline__ void init(uint32_t d, uint64_t pos) const {
         lcur[d] = pos;
@@ -168,6 +170,29 @@ struct Emit {
             const uint64_t lc = lcur[d];
             dl[d] = lc - lstart[d];
             lim[d] = TAILS ? flush_end(lc + hist[d], last) : ~0ull;
+        }
+    }
+    // While ranking a tile: the record whose rank completes destination d's
+    // pending tail segment lists d for flush_listed() (not on the chunk's
+    // last tile, where every pending tail is flushed)
+    __device__ __forceinline__ void note(uint32_t d, uint32_t rank, bool last) const {
+        if (!TAILS || last) return;
+        const uint32_t need = (0u - (uint32_t)lcur[d]) & (SEG - 1);
+        if (need && rank == need - 1) flist[atomicAdd(nflush, 1u)] = (uint16_t)d;
+    }
+    // flush_tails() over the listed destinations only
+    __device__ __forceinline__ void flush_listed(uint32_t F, bool last, T *out) const {
+        if (!TAILS) return;
+        if (last) {
+            flush_tails(F, last, out);
+            return;
+        }
+        const uint32_t n = *nflush * SEG;
+        for (uint32_t x = threadIdx.x; x < n; x += blockDim.x) {
+            const uint32_t d = flist[x / SEG], sl = x % SEG;
+            const uint64_t lc = lcur[d];
+            const uint64_t a = lc & ~(uint64_t)(SEG - 1);
+            if (sl >= hskip[d] && a + sl < lc) out[a + sl] = tail[d * SEG + sl];
         }
     }
     // phase 2 (after a barrier): staged record q of destination d, from the
@@ -199,6 +224,7 @@ struct Emit {
             lcur[d] = e;
             hist[d] = 0;
         }
+        if (nflush && threadIdx.x == 0) *nflush = 0;
     }
 };
 
@@ -277,7 +303,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
     uint8_t *hskip = (uint8_t *)(s_wtot + 16);        // [F1]
     uint64_t *s_meta = (uint64_t *)(hskip + ((F1a + 7) & ~7u));
     uint64_t *s_koff = s_meta + 2;
-    const Emit<uint64_t, SEG> em{lcur, hskip, tail, hist, lstart, nullptr, nullptr};
+    const Emit<uint64_t, SEG> em{lcur, hskip, tail, hist, lstart, nullptr, nullptr, nullptr, nullptr};
     const int shift = P.s0 + P.s2;
     const uint64_t omask = (1ull << shift) - 1;
     constexpr int TILE_KMERS = L1_THREADS * KPT;
@@ -452,26 +478,29 @@ __global__ void k_off2(uint32_t F1, int s2, const uint64_t *off1, const uint32_t
 // tile are written together, so L2 completes their lines; only whole aligned
 // 128-B segments (SEG = 16 records) are written, remainders wait in LDS tails
 // (random 128-B runs stream at ~5 TB/s on MI355X, 64-B runs at ~3 TB/s).
-template <int THREADS, int SEG>
+template <int THREADS, int SEG, int RPT>
 __global__ void __launch_bounds__(THREADS) k_scatter_l2(uint32_t F1, int s0, int s2, const uint64_t *off1,
                                                         const uint32_t *ch2, const uint64_t *O2,
                                                         const uint64_t *rec_in, uint64_t *rec_out) {
-    constexpr int TILE = THREADS * PT_RPT;
+    constexpr int TILE = THREADS * RPT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t F2 = 1u << s2;
     uint64_t *lcur = (uint64_t *)smem;             // [F2]
     uint64_t *tail = lcur + F2;                    // [F2*SEG]
     uint32_t *hist = (uint32_t *)(tail + F2 * SEG);  // [F2]
-    uint8_t *hskip = (uint8_t *)(hist + F2);       // [F2]
-    const Emit<uint64_t, SEG> em{lcur, hskip, tail, hist, nullptr, nullptr, nullptr};
+    uint32_t *nflush = hist + F2;                  // [2]
+    uint16_t *flist = (uint16_t *)(nflush + 2);    // [F2]
+    uint8_t *hskip = (uint8_t *)(flist + ((F2 + 1) & ~1u));  // [F2]
+    const Emit<uint64_t, SEG> em{lcur, hskip, tail, hist, nullptr, nullptr, nullptr, flist, nflush};
     const uint64_t rmask = (1ull << s0) - 1;
     L2Chunk k;
     if (!l2_chunk(F1, off1, ch2, &k)) return;
     const uint64_t base = (uint64_t)ch2[k.b] * F2 + k.c;
     for (uint32_t r = threadIdx.x; r < F2; r += THREADS) em.init(r, O2[base + (uint64_t)r * k.nc]);
-    uint64_t v[PT_RPT];
+    if (threadIdx.x == 0) *nflush = 0;
+    uint64_t v[RPT];
 #pragma unroll
-    for (int q = 0; q < PT_RPT; q++) {
+    for (int q = 0; q < RPT; q++) {
         const uint64_t idx = k.r0 + (uint64_t)q * THREADS + threadIdx.x;
         v[q] = idx < min(k.r1, k.r0 + TILE) ? rec_in[idx] : ~0ull;
     }
@@ -480,26 +509,29 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2(uint32_t F1, int s0, int
         const uint64_t t0 = k.r0 + (uint64_t)ti * TILE;
         const bool last = ti + 1 == ntiles;
         block_sync();
-        uint32_t rank[PT_RPT];
-        uint64_t x[PT_RPT];
+        uint32_t rank[RPT];
+        uint64_t x[RPT];
 #pragma unroll
-        for (int q = 0; q < PT_RPT; q++) {
+        for (int q = 0; q < RPT; q++) {
             x[q] = v[q];
-            if (x[q] != ~0ull) rank[q] = atomicAdd(&hist[(uint32_t)x[q] >> s0], 1u);
+            if (x[q] != ~0ull) {
+                rank[q] = atomicAdd(&hist[(uint32_t)x[q] >> s0], 1u);
+                em.note((uint32_t)x[q] >> s0, rank[q], last);
+            }
         }
         {
             const uint64_t n0 = t0 + TILE, n1 = min(k.r1, n0 + TILE);
 #pragma unroll
-            for (int q = 0; q < PT_RPT; q++) {
+            for (int q = 0; q < RPT; q++) {
                 const uint64_t idx = n0 + (uint64_t)q * THREADS + threadIdx.x;
                 v[q] = idx < n1 ? rec_in[idx] : ~0ull;
             }
         }
         block_sync();
-        em.flush_tails(F2, last, rec_out);
+        em.flush_listed(F2, last, rec_out);
         block_sync();
 #pragma unroll
-        for (int q = 0; q < PT_RPT; q++)
+        for (int q = 0; q < RPT; q++)
             if (x[q] != ~0ull)
                 em.put_rank((uint32_t)x[q] >> s0, rank[q], (x[q] & ~0xFFFFFFFFull) | (x[q] & rmask), last, rec_out);
         block_sync();

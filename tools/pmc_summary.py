@@ -59,17 +59,26 @@ def main():
         wr.writeheader()
         wr.writerows(rows)
     dom = bench["roofline"]["kernel"]
-    match = [r for r in rows if r["kernel"].split("<")[0].endswith("k_" + dom.split("_byte")[0].split("_nibble")[0].split("_bit")[0])
-             or r["kernel"].endswith(dom)]
-    if match:
-        r = match[0]
-        json.dump({"kernel": dom, "device_kernel": r["kernel"], "config": bench["config"]["workload"],
-                   "hbm_bytes_per_launch": r["hbm_bytes_per_launch"],
-                   "fetch_kib_raw_per_launch": r["fetch_kib_raw_per_launch"],
-                   "write_kib_per_launch": r["write_kib_per_launch"],
-                   "note": "FETCH_SIZE doubled per the gfx950 calibration; tag %s" % tag},
-                  open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
-    print("dominant", dom, "match", match[:1])
+    per = {timer_name(r["kernel"]): r["hbm_bytes_per_launch"] for r in rows}
+    json.dump({"kernel": dom, "config": bench["config"]["workload"],
+               "hbm_bytes_per_launch": per.get(dom),
+               "kernels": per,
+               "note": "HBM bytes per launch (FETCH_SIZE doubled per the gfx950 calibration + WRITE_SIZE), "
+                       "keyed by the engine's kernel timer names; tag %s" % tag},
+              open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+    print("dominant", dom, per.get(dom))
+
+
+def timer_name(device_kernel):
+    """kh::k_apply_count<1> -> apply_byte, kh::k_scatter_l1<...> -> scatter_l1 (kh_engine.hip TIMED names)."""
+    base = device_kernel.split("<")[0].split("::")[-1]
+    if base.startswith("k_"):
+        base = base[2:]
+    if base == "apply_count":
+        return {"1": "apply_byte", "7": "apply_nibble"}.get(device_kernel.split("<")[1].split(">")[0], base)
+    if base == "apply_bit":
+        return "apply_bit"
+    return base
 
 
 if __name__ == "__main__":
