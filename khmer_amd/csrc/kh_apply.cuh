@@ -204,18 +204,33 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
         PH(0);
         // records: the prefetched batch, then APPLY_RECS loads in flight per thread
         if (!(P.ablate & 2)) {
+            // two batches of APPLY_RECS loads in flight: batch k+1 is issued
+            // before batch k's atomics, so each wait is for the older batch only
+            const uint64_t step = (uint64_t)APPLY_RECS * APPLY_THREADS;
+            uint64_t va[APPLY_RECS], vb[APPLY_RECS];
+            uint64_t q0 = ri.e0 + step + t;
+#pragma unroll
+            for (int u = 0; u < APPLY_RECS; u++) {
+                const uint64_t q = q0 + (uint64_t)u * APPLY_THREADS;
+                va[u] = q < ri.e1 ? A.rec[q] : ~0ull;
+            }
 #pragma unroll
             for (int u = 0; u < APPLY_RECS; u++) count_record(cur.v[u], cnt, minj);
-            const uint64_t step = (uint64_t)APPLY_RECS * APPLY_THREADS;
-            for (uint64_t q0 = ri.e0 + step + t; q0 < ri.e1; q0 += step) {
-                uint64_t v[APPLY_RECS];
+            for (; q0 < ri.e1; q0 += 2 * step) {
 #pragma unroll
                 for (int u = 0; u < APPLY_RECS; u++) {
-                    const uint64_t q = q0 + (uint64_t)u * APPLY_THREADS;
-                    v[u] = q < ri.e1 ? A.rec[q] : ~0ull;
+                    const uint64_t q = q0 + step + (uint64_t)u * APPLY_THREADS;
+                    vb[u] = q < ri.e1 ? A.rec[q] : ~0ull;
                 }
 #pragma unroll
-                for (int u = 0; u < APPLY_RECS; u++) count_record(v[u], cnt, minj);
+                for (int u = 0; u < APPLY_RECS; u++) count_record(va[u], cnt, minj);
+#pragma unroll
+                for (int u = 0; u < APPLY_RECS; u++) {
+                    const uint64_t q = q0 + 2 * step + (uint64_t)u * APPLY_THREADS;
+                    va[u] = q < ri.e1 ? A.rec[q] : ~0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < APPLY_RECS; u++) count_record(vb[u], cnt, minj);
             }
         }
         block_sync();
