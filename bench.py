@@ -58,7 +58,9 @@ def parse():
     ap.add_argument("-k", type=int, default=None, help="override the preset's k")
     ap.add_argument("--tables", type=int, default=4)
     ap.add_argument("-x", type=float, default=None, help="override the preset's table size")
-    ap.add_argument("--batch-kmers", type=int, default=1 << 30)
+    ap.add_argument("--batch-kmers", type=int, default=2560 << 20,
+                    help="largest device pass (the library cap, MAX_PASS_KMERS); fewer, larger passes "
+                         "amortise the per-bin work of every pass")
     ap.add_argument("--no-bigcount", action="store_true")
     ap.add_argument("--ablate", type=int, default=0,
                     help="timing-only KH_ABLATE bits (results become wrong; never for reported numbers)")

@@ -43,16 +43,33 @@ struct RegionInfo {
     uint64_t e0, e1, bin_lo;
 };
 
-// region rr (in apply order: table by table) -> table, bins, record range
-__device__ __forceinline__ RegionInfo region_info(const Params &P, const ApplyArgs &A, uint64_t rr) {
-    RegionInfo ri;
+// record range of region rr (in apply order: table by table); loaded one
+// region ahead of its prefetch so the prefetch never waits for it
+struct Bounds {
+    uint64_t e0, e1;
+};
+__device__ __forceinline__ uint64_t region_index(const Params &P, const ApplyArgs &A, uint64_t rr, int *ti) {
     int i = 0;
     while (i + 1 < P.n && rr >= A.rprefix[i + 1]) i++;
+    *ti = i;
+    return (P.tbase[i] >> P.s0) + (rr - A.rprefix[i]);
+}
+__device__ __forceinline__ Bounds load_bounds(const Params &P, const ApplyArgs &A, uint64_t rr, uint64_t total) {
+    if (rr >= total) return Bounds{0, 0};
+    int i;
+    const uint64_t region = region_index(P, A, rr, &i);
+    return Bounds{A.off2[region], A.off2[region + 1]};
+}
+
+// region rr -> table, bins, record range
+__device__ __forceinline__ RegionInfo region_info(const Params &P, const ApplyArgs &A, uint64_t rr, Bounds b) {
+    RegionInfo ri;
+    int i;
+    region_index(P, A, rr, &i);
     const uint64_t lreg = rr - A.rprefix[i];
-    const uint64_t region = (P.tbase[i] >> P.s0) + lreg;
     ri.i = i;
-    ri.e0 = A.off2[region];
-    ri.e1 = A.off2[region + 1];
+    ri.e0 = b.e0;
+    ri.e1 = b.e1;
     ri.bin_lo = lreg << P.s0;
     ri.nb = (uint32_t)min((uint64_t)1 << P.s0, P.lsz[i] - ri.bin_lo);
     return ri;
@@ -67,10 +84,10 @@ struct Prefetch {
 
 template <int KIND>
 __device__ __forceinline__ void prefetch_region(const Params &P, const ApplyArgs &A, uint64_t rr, uint64_t total,
-                                                Prefetch &f) {
+                                                Bounds b, Prefetch &f) {
     // every field is written on every path (keeps the struct in registers)
     const bool valid = rr < total;
-    f.ri = region_info(P, A, valid ? rr : 0);
+    f.ri = region_info(P, A, valid ? rr : 0, b);
     if (!valid) f.ri.e1 = f.ri.e0;
     f.tv = make_uint4(0, 0, 0, 0);
     const uint32_t t = threadIdx.x;
@@ -152,7 +169,8 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
     uint64_t occ = 0;
     const uint64_t total = A.rprefix[P.n];
     Prefetch cur, nxt;
-    prefetch_region<KIND>(P, A, blockIdx.x, total, cur);
+    prefetch_region<KIND>(P, A, blockIdx.x, total, load_bounds(P, A, blockIdx.x, total), cur);
+    Bounds bnext = load_bounds(P, A, blockIdx.x + gridDim.x, total);
 #ifdef KH_PHASES
     uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
     uint64_t tA = __builtin_amdgcn_s_memtime(), tB;
@@ -164,9 +182,11 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
         const RegionInfo ri = cur.ri;
         if (ri.e0 == ri.e1) {
             if (t == 0) A.wcnt[rr] = 0;
-            prefetch_region<KIND>(P, A, rr + gridDim.x, total, cur);
+            prefetch_region<KIND>(P, A, rr + gridDim.x, total, bnext, cur);
+            bnext = load_bounds(P, A, rr + 2 * (uint64_t)gridDim.x, total);
             continue;
         }
+        const Bounds bafter = load_bounds(P, A, rr + 2 * (uint64_t)gridDim.x, total);
         const uint32_t nb = ri.nb;
         const uint32_t nchunk = (nb + 15) / 16;   // 16 bins per chunk
         uint8_t *tab = A.tab + P.tbyte[ri.i];
@@ -264,7 +284,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
                 if (c == 0) win |= 1u << k;
                 else inval |= 1u << k;
                 if (bigc && c == 255) full |= 1u << k;
-                if (bigc && c < 255 && v > 255) {   // insert r sees c + r: full iff c + r >= 255, r < n
+                if (bigc && c < 255 && v > 255 && !(P.ablate & 8)) {   // insert r sees c + r: full iff c + r >= 255, r < n
                     const uint64_t idx = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
                     if (idx < A.cap_cross) A.cross[idx] = ((P.tbase[ri.i] + ri.bin_lo + o + k) << 8) | c;
                     else atomicOr((unsigned long long *)&A.ctr[CTR_ERR], 1ull);
@@ -301,10 +321,12 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
             }
         }
         if (P.ablate & 1) nw = 0;
+        PH(4);
         const uint32_t wex = wave_winner_scan(nw, s_wt);
         block_sync();
         PH(2);
-        prefetch_region<KIND>(P, A, rr + gridDim.x, total, nxt);
+        prefetch_region<KIND>(P, A, rr + gridDim.x, total, bnext, nxt);
+        bnext = bafter;
         // pass 2: write back changed 16-bin chunks; winners to the region's segment
         for (uint32_t x = t; x < nchunk; x += blockDim.x) {
             if (!((chg[x >> 5] >> (x & 31)) & 1) || (P.ablate & 4)) continue;
@@ -380,14 +402,17 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyA
     uint64_t occ = 0;
     const uint64_t total = A.rprefix[P.n];
     Prefetch cur, nxt;
-    prefetch_region<BIT>(P, A, blockIdx.x, total, cur);
+    prefetch_region<BIT>(P, A, blockIdx.x, total, load_bounds(P, A, blockIdx.x, total), cur);
+    Bounds bnext = load_bounds(P, A, blockIdx.x + gridDim.x, total);
     for (uint64_t rr = blockIdx.x; rr < total; rr += gridDim.x) {
         const RegionInfo ri = cur.ri;
         if (ri.e0 == ri.e1) {
             if (t == 0) A.wcnt[rr] = 0;
-            prefetch_region<BIT>(P, A, rr + gridDim.x, total, cur);
+            prefetch_region<BIT>(P, A, rr + gridDim.x, total, bnext, cur);
+            bnext = load_bounds(P, A, rr + 2 * (uint64_t)gridDim.x, total);
             continue;
         }
+        const Bounds bafter = load_bounds(P, A, rr + 2 * (uint64_t)gridDim.x, total);
         const uint32_t nb = ri.nb;
         const uint32_t nchunk = (nb + 127) / 128;   // 16 bytes = 128 bins per chunk
         uint8_t *tab = A.tab + P.tbyte[ri.i] + (ri.bin_lo >> 3);
@@ -395,21 +420,37 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyA
         for (uint32_t x = t; x < nchunk * 32; x += blockDim.x) ((uint4 *)minj)[x] = make_uint4(NO_J, NO_J, NO_J, NO_J);
         if (t < 4) chg[t] = 0;
         block_sync();
-#pragma unroll
-        for (int u = 0; u < APPLY_RECS; u++) bit_record(cur.v[u], minj);
-        const uint64_t step = (uint64_t)APPLY_RECS * APPLY_THREADS;
-        for (uint64_t q0 = ri.e0 + step + t; q0 < ri.e1; q0 += step) {
-            uint64_t v[APPLY_RECS];
+        {
+            const uint64_t step = (uint64_t)APPLY_RECS * APPLY_THREADS;
+            uint64_t va[APPLY_RECS], vb[APPLY_RECS];
+            uint64_t q0 = ri.e0 + step + t;
 #pragma unroll
             for (int u = 0; u < APPLY_RECS; u++) {
                 const uint64_t q = q0 + (uint64_t)u * APPLY_THREADS;
-                v[u] = q < ri.e1 ? A.rec[q] : ~0ull;
+                va[u] = q < ri.e1 ? A.rec[q] : ~0ull;
             }
 #pragma unroll
-            for (int u = 0; u < APPLY_RECS; u++) bit_record(v[u], minj);
+            for (int u = 0; u < APPLY_RECS; u++) bit_record(cur.v[u], minj);
+            for (; q0 < ri.e1; q0 += 2 * step) {
+#pragma unroll
+                for (int u = 0; u < APPLY_RECS; u++) {
+                    const uint64_t q = q0 + step + (uint64_t)u * APPLY_THREADS;
+                    vb[u] = q < ri.e1 ? A.rec[q] : ~0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < APPLY_RECS; u++) bit_record(va[u], minj);
+#pragma unroll
+                for (int u = 0; u < APPLY_RECS; u++) {
+                    const uint64_t q = q0 + 2 * step + (uint64_t)u * APPLY_THREADS;
+                    va[u] = q < ri.e1 ? A.rec[q] : ~0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < APPLY_RECS; u++) bit_record(vb[u], minj);
+            }
         }
         block_sync();
-        prefetch_region<BIT>(P, A, rr + gridDim.x, total, nxt);
+        prefetch_region<BIT>(P, A, rr + gridDim.x, total, bnext, nxt);
+        bnext = bafter;
         // pass 1 (thread per bin): winners set their bit
         uint32_t nw = 0;
         const uint32_t lane = t & 63;
@@ -466,7 +507,7 @@ __device__ __forceinline__ uint32_t w_chunk_setup(const Params &P, const ApplyAr
     if (threadIdx.x < W_RPC) {
         const uint64_t rr = rr0 + threadIdx.x;
         const uint32_t c = rr < total ? A.wcnt[rr] : 0;
-        s_e0[threadIdx.x] = c ? region_info(P, A, rr).e0 : 0;
+        s_e0[threadIdx.x] = c ? load_bounds(P, A, rr, A.rprefix[P.n]).e0 : 0;
         const uint32_t lane = threadIdx.x;
         uint32_t incl = c;
         for (int d = 1; d < 64; d <<= 1) {

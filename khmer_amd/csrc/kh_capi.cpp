@@ -223,7 +223,7 @@ int kh_graph_n_occupied(kh_graph *h, uint64_t *out) {
 int kh_graph_set_batch_kmers(kh_graph *h, uint64_t max_kmers) {
     return guard([&] {
         CHECK_PTR(h);
-        if (max_kmers < 1024 || max_kmers > (1ull << 31)) fail(KH_EVALUE, "batch size out of range");
+        if (max_kmers < 1024 || max_kmers > MAX_PASS_KMERS) fail(KH_EVALUE, "batch size out of range");
         h->g->batch_kmers = max_kmers;
     });
 }

@@ -69,7 +69,7 @@ static PassGeo pass_geo(const Params &P, uint64_t nkmers) {
     q.ck1 = 32768u * ((P.F1 + 1023) / 1024);
     q.nch1 = (uint32_t)((nkmers + q.ck1 - 1) / q.ck1);
     q.nch2max = q.recs / L2_CHUNK + P.F1 + 1;
-    q.js = std::max(17, ceil_log2(nkmers) - 11);   // <= 2048 windows of <= 2^20 k-mers
+    q.js = std::min(20, std::max(17, ceil_log2(nkmers) - 11));   // <= 2560 windows of <= 2^20 k-mers
     q.FJ = (uint32_t)((nkmers + (1ull << q.js) - 1) >> q.js);
     q.regions = 0;
     for (int i = 0; i < P.n; i++) q.regions += (P.lsz[i] + (1ull << P.s0) - 1) >> P.s0;
@@ -88,15 +88,6 @@ static void ws_prepare(Graph *g, const PassGeo &q) {
         w.fullf = nullptr;
         KH_HIP(hipMalloc((void **)&w.fullf, cap + 64));
         w.cap_kmers = cap;
-    }
-    if (q.recs > w.cap_recs) {
-        uint64_t cap = std::max<uint64_t>(q.recs, w.cap_recs + w.cap_recs / 2);
-        for (uint64_t **pp : {&w.rec1, &w.rec2}) {
-            if (*pp) KH_HIP(hipFree(*pp));
-            *pp = nullptr;
-            KH_HIP(hipMalloc((void **)pp, cap * 8 + 64));
-        }
-        w.cap_recs = cap;
     }
     ensure((void **)&w.mcnt, &w.cap_m, q.mcnt, 4);
     ensure((void **)&w.moff, &w.cap_moff, q.mcnt, 8);
@@ -124,6 +115,22 @@ static void ws_prepare(Graph *g, const PassGeo &q) {
         w.cap_bc = 1 << 22;
         KH_HIP(hipMalloc((void **)&w.bc, w.cap_bc * 8));
     }
+}
+
+// record buffers for a pass holding `recs` records (level-1 out / level-2 out;
+// the dead level-1 buffer later holds the winner lists).  Sized from the
+// device's exact count, so a shard only holds the records it owns.
+static void ensure_recs(Graph *g, uint64_t recs) {
+    Workspace &w = g->ws;
+    if (recs <= w.cap_recs && w.rec1) return;
+    uint64_t cap = std::max<uint64_t>(recs, w.cap_recs + w.cap_recs / 2);
+    cap = std::max<uint64_t>(cap, 1024);
+    for (uint64_t **pp : {&w.rec1, &w.rec2}) {
+        if (*pp) KH_HIP(hipFree(*pp));
+        *pp = nullptr;
+        KH_HIP(hipMalloc((void **)pp, cap * 8 + 64));
+    }
+    w.cap_recs = cap;
 }
 
 // KH_CHECK (development): record buffers pre-filled with a sentinel; after
@@ -301,7 +308,7 @@ struct PassState {
 
 template <class Src>
 static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
-    if (nkmers > (1ull << 31)) fail(KH_EVALUE, "device batch too large (more than 2^31 k-mers)");
+    if (nkmers > MAX_PASS_KMERS) fail(KH_EVALUE, "device batch too large (more than 2560 * 2^20 k-mers)");
     const Params &P = g->prm;
     PassState ps;
     ps.q = pass_geo(P, nkmers);
@@ -321,10 +328,6 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
 
     KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
     if (bigc) KH_HIP(hipMemsetAsync(w.fullf, 0, flag_bytes, st));
-    if (check_mode()) {
-        KH_HIP(hipMemsetAsync(w.rec1, 0xFF, q.recs * 8, st));
-        KH_HIP(hipMemsetAsync(w.rec2, 0xFF, q.recs * 8, st));
-    }
 
     // level 1
     TIMED("hist_l1", hipLaunchKernelGGL(k_hist_l1<Src>, dim3(q.nch1), dim3(L1_THREADS), lds_hist_l1(P, window), st, P,
@@ -332,6 +335,15 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     TIMED("scan", scan_counts(g, w.mcnt, w.moff, F1 * q.nch1));
     TIMED("plan_l2", hipLaunchKernelGGL(k_plan_l2, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1, q.nch1,
                                         w.moff, w.mcnt, w.off1, w.ch2));
+    // records this pass writes (all of them on one device; the owned ones on a shard)
+    uint64_t nrec = 0;
+    KH_HIP(hipMemcpyAsync(&nrec, w.off1 + F1, 8, hipMemcpyDeviceToHost, st));
+    KH_HIP(hipStreamSynchronize(st));
+    ensure_recs(g, nrec);
+    if (check_mode()) {
+        KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
+        KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
+    }
     for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
         const int nt = std::min(L1_MAX_RPT, P.n - t0);
         const int kpt = std::max(1, L1_MAX_RPT / nt);
@@ -340,7 +352,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                                                lds_scatter_l1(P, window, tile_kmers), st, P, src, nkmers, q.ck1,
                                                q.nch1, t0, nt, w.moff, w.rec1));
     }
-    if (check_mode()) check_holes(g, w.rec1, q.recs, "scatter_l1");
+    if (check_mode()) check_holes(g, w.rec1, nrec, "scatter_l1");
     // level 2
     const unsigned g2 = (unsigned)q.nch2max;
     TIMED("hist_l2", hipLaunchKernelGGL(k_hist_l2, dim3(g2), dim3(PT_THREADS), F2 * 4, st, (uint32_t)F1, P.s0, P.s2,
@@ -352,7 +364,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                                            lds_scatter_l2(P), st, (uint32_t)F1, P.s0, P.s2, w.off1, w.ch2, w.moff,
                                            w.rec1, w.rec2));
 
-    if (check_mode()) check_holes(g, w.rec2, q.recs, "scatter_l2");
+    if (check_mode()) check_holes(g, w.rec2, nrec, "scatter_l2");
     // apply (winner segments -> first half of the dead level-1 buffer)
     uint32_t *win = (uint32_t *)w.rec1;
     uint32_t *wout = win + w.cap_recs;
@@ -481,12 +493,14 @@ static void consume_reads(Graph *g, Src base, const uint64_t *d_koff, uint64_t n
     base.nreads = nreads;
     base.kbase = 0;
     base.rbase = 0;
-    if (out || nkmers <= std::min<uint64_t>(B + (B >> 4), 1ull << 31)) {   // one pass (koff[0] == 0 by contract)
+    if (out || nkmers <= std::min<uint64_t>(B + (B >> 4), MAX_PASS_KMERS)) {   // one pass (koff[0] == 0 by contract)
         run_pass(g, base, nkmers, out);
         return;
     }
-    if (kpr) {   // fixed-length reads: batches of whole reads, no offsets needed
-        const uint64_t rpb = std::max<uint64_t>(1, B / kpr);
+    if (kpr) {   // fixed-length reads: equal batches of whole reads, no offsets needed
+        const uint64_t rpb0 = std::max<uint64_t>(1, std::min(B, MAX_PASS_KMERS) / kpr);
+        const uint64_t npass = (nreads + rpb0 - 1) / rpb0;
+        const uint64_t rpb = (nreads + npass - 1) / npass;
         for (uint64_t r0 = 0; r0 < nreads; r0 += rpb) {
             Src s = base;
             s.kbase = r0 * kpr;
@@ -494,12 +508,14 @@ static void consume_reads(Graph *g, Src base, const uint64_t *d_koff, uint64_t n
         }
         return;
     }
-    const uint64_t nchunks = (nkmers + B - 1) / B;
+    const uint64_t B0 = std::min(B, MAX_PASS_KMERS);
+    const uint64_t nchunks = (nkmers + B0 - 1) / B0;
+    const uint64_t Bb = (nkmers + nchunks - 1) / nchunks;   // equal passes
     std::vector<uint64_t> rr(nchunks + 1), kk(nchunks + 1);
     uint64_t *d = nullptr;
     KH_HIP(hipMalloc((void **)&d, (nchunks + 1) * 16));
     hipLaunchKernelGGL(k_chunk_bounds, dim3((unsigned)std::min<uint64_t>((nchunks + 256) / 256, 4096)), dim3(256), 0,
-                       g->stream, d_koff, nreads, B, nchunks, d, d + nchunks + 1);
+                       g->stream, d_koff, nreads, Bb, nchunks, d, d + nchunks + 1);
     KH_HIP(hipGetLastError());
     KH_HIP(hipMemcpyAsync(rr.data(), d, (nchunks + 1) * 8, hipMemcpyDeviceToHost, g->stream));
     KH_HIP(hipMemcpyAsync(kk.data(), d + nchunks + 1, (nchunks + 1) * 8, hipMemcpyDeviceToHost, g->stream));
@@ -1152,7 +1168,9 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
     }
     const uint64_t kpr = read_len - k + 1;
     const uint64_t nwords = (nreads * read_len + 31) / 32 + 1;
-    const uint64_t rpb = std::max<uint64_t>(1, std::min<uint64_t>(g0->batch_kmers, 1ull << 31) / kpr);
+    const uint64_t rpb0 = std::max<uint64_t>(1, std::min<uint64_t>(g0->batch_kmers, MAX_PASS_KMERS) / kpr);
+    const uint64_t npass = std::max<uint64_t>(1, (nreads + rpb0 - 1) / rpb0);
+    const uint64_t rpb = std::max<uint64_t>(1, (nreads + npass - 1) / npass);   // equal passes
     for (int s = 0; s < W; s++) {
         std::vector<const uint64_t *> buf(NL);
         if (G->comm) {

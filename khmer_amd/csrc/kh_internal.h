@@ -35,6 +35,10 @@ struct Error : std::runtime_error {
     } while (0)
 
 constexpr int MAXT = 32;  // tables per graph on device (NibbleStorage's own cap, storage.hh:290)
+// k-mers of one device pass: at most 2560 winner windows of 2^20 k-mers (the
+// LDS of k_scatter_w's per-window tails and k_mark's 2^20-bit bitmap); batch
+// k-mer indices stay 32-bit
+constexpr uint64_t MAX_PASS_KMERS = 2560ull << 20;
 
 // ---- partition geometry -----------------------------------------------------
 // Every table bin gets a global id G = tbase[i] + bin.  Regions are 2^s0 bins
