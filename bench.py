@@ -9,10 +9,11 @@ The reads are generated straight into HBM before timing
 the tables, then consume every read (hash -> partition -> LDS apply ->
 finalize), i.e. the whole hot path over the whole batch.
 
-Multi-GPU (torchrun, one rank per GPU): tables shard by bin residue
-(bin % world == rank); every rank generates its own 50M reads
-(weak scaling), hashes them, and exchanges (table, bin) records with RCCL
-all-to-all over xGMI; owners apply them.  value = all ranks' k-mers / max time.
+Multi-GPU (torchrun, one rank per GPU): every table is split into G
+contiguous bin ranges, one per rank.  Every rank generates
+its own 50M reads (weak scaling); each rank's packed reads are broadcast over
+RCCL/xGMI, every rank hashes every k-mer and applies only the inserts whose
+bins it owns (Option B).  value = all ranks' k-mers / max time.
 
 Prints ONE JSON line (rank 0).
 """
