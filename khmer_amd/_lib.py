@@ -9,7 +9,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkhmer_hip.so")
+LIB_PATH = os.environ.get("KHMER_AMD_LIB") or os.path.join(_HERE, "libkhmer_hip.so")   # override: development builds
 
 KH_OK, KH_EVALUE, KH_EFILE, KH_EATTR, KH_ENOMEM, KH_EDEVICE, KH_ERUNTIME, KH_END = range(8)
 STORAGE_BYTE, STORAGE_BIT, STORAGE_NIBBLE = 1, 2, 7

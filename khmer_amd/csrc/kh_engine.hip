@@ -265,8 +265,9 @@ static L1Fn<Src> l1_kernel(bool seg, int kpt) {
     }
 }
 
-// LDS footprints
 static size_t lds_window(bool window, int tile_kmers) { return 16 + (window ? (size_t)(tile_kmers + 2) * 8 : 0); }
+
+// LDS footprints
 static size_t lds_hist_l1(const Params &P, bool window) {
     return (size_t)((P.F1 + 3) & ~3u) * 4 + lds_window(window, L1_HIST_TILE);
 }
@@ -290,6 +291,63 @@ static size_t lds_scatter_w(uint32_t FJ) {
 static size_t lds_apply(const Params &P) {
     const size_t R = (size_t)1 << P.s0;
     return P.kind == BIT ? R * 4 + 16 + 64 + R / 8 : R * 4 * 2 + (R / 512) * 4 + 64 + R / 8 + 16 + R + R / 4;
+}
+
+// A shard's level 1 through k_own_filter (kh_partition.cuh) when it owns a
+// small share of the bins: a group of >= KH_OWN_FILTER_MIN ranks (default 3;
+// 0 disables), local bin ids below 2^32 and at most 1024 level-1 buckets.
+static bool use_own_filter(const Graph *g) {
+    static const int min_world = [] {
+        const char *e = getenv("KH_OWN_FILTER_MIN");
+        return e && *e ? atoi(e) : 3;
+    }();
+    const Params &P = g->prm;
+    return min_world > 0 && g->world >= min_world && P.F1 <= 1024 &&
+           ((uint64_t)P.F1 << (P.s0 + P.s2)) <= (1ull << 32);
+}
+static size_t lds_scatter_rec(uint64_t F) {
+    const size_t Fa = (F + 3) & ~3ull;
+    return Fa * 8 + Fa * 8 * L2_SEG + Fa * 4 + 16 + Fa * 2 + Fa;
+}
+template <class Src, int KPT>
+static void launch_own_filter(Graph *g, const Src &src, uint64_t nkmers, bool window, int t0, int nt) {
+    constexpr uint32_t CK = 32768;
+    const uint32_t nch = (uint32_t)((nkmers + CK - 1) / CK);
+    const size_t lds = (size_t)OWN_BUF * 8 + 16 * 4 + 8 + lds_window(window, L1_THREADS * KPT);
+    hipLaunchKernelGGL((k_own_filter<Src, KPT>), dim3(nch), dim3(L1_THREADS), lds, g->stream, g->prm, src, nkmers,
+                       CK, t0, nt, g->ws.cap_frec, g->ws.frec, g->ws.fcount);
+}
+// owned records of the pass into ws.frec (grown and re-run when the estimate
+// was short); returns their number
+template <class Src>
+static uint64_t own_filter(Graph *g, const Src &src, uint64_t nkmers, bool window) {
+    const Params &P = g->prm;
+    Workspace &w = g->ws;
+    double expect = 0;
+    for (int i = 0; i < P.n; i++) expect += (double)nkmers * (double)P.lsz[i] / (double)P.p[i];
+    const uint64_t want = (uint64_t)(expect * 1.05) + (1u << 20);
+    ensure((void **)&w.frec, &w.cap_frec, want, 8);
+    if (!w.fcount) KH_HIP(hipMalloc((void **)&w.fcount, 64));
+    for (int attempt = 0;; attempt++) {
+        KH_HIP(hipMemsetAsync(w.fcount, 0, 8, g->stream));
+        for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
+            const int nt = std::min(L1_MAX_RPT, P.n - t0);
+            int kpt = 1;
+            while (kpt * 2 * nt <= L1_MAX_RPT) kpt *= 2;
+            TIMED("own_filter", switch (kpt) {
+                case 8: launch_own_filter<Src, 8>(g, src, nkmers, window, t0, nt); break;
+                case 4: launch_own_filter<Src, 4>(g, src, nkmers, window, t0, nt); break;
+                case 2: launch_own_filter<Src, 2>(g, src, nkmers, window, t0, nt); break;
+                default: launch_own_filter<Src, 1>(g, src, nkmers, window, t0, nt); break;
+            });
+        }
+        unsigned long long cnt = 0;
+        KH_HIP(hipMemcpyAsync(&cnt, w.fcount, 8, hipMemcpyDeviceToHost, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+        if (cnt <= w.cap_frec) return cnt;
+        if (attempt) fail(KH_EDEVICE, "owned-record filter overflowed twice");
+        ensure((void **)&w.frec, &w.cap_frec, cnt, 8);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -330,13 +388,32 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     if (bigc) KH_HIP(hipMemsetAsync(w.fullf, 0, flag_bytes, st));
 
     // level 1
+    uint64_t nrec = 0;   // records this pass writes (all on one device; the owned ones on a shard)
+    if (use_own_filter(g)) {
+        nrec = own_filter(g, src, nkmers, window);
+        const uint32_t nch = (uint32_t)std::max<uint64_t>(1, (nrec + L2_CHUNK - 1) / L2_CHUNK);
+        ensure((void **)&w.mcnt, &w.cap_m, F1 * nch, 4);
+        ensure((void **)&w.moff, &w.cap_moff, F1 * nch, 8);
+        const int shift = P.s0 + P.s2;
+        TIMED("hist_rec", hipLaunchKernelGGL(k_hist_rec, dim3(nch), dim3(PT_THREADS), F1 * 4, st, w.frec, nrec,
+                                             (uint32_t)F1, shift, nch, w.mcnt));
+        TIMED("scan", scan_counts(g, w.mcnt, w.moff, F1 * nch));
+        TIMED("plan_l2", hipLaunchKernelGGL(k_plan_l2, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1,
+                                            nch, w.moff, w.mcnt, w.off1, w.ch2));
+        ensure_recs(g, nrec);
+        if (check_mode()) {
+            KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
+            KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
+        }
+        TIMED("scatter_rec", hipLaunchKernelGGL((k_scatter_rec<PT_THREADS, L2_SEG, L2_RPT>), dim3(nch),
+                                                dim3(PT_THREADS), lds_scatter_rec(F1), st, w.frec, nrec,
+                                                (uint32_t)F1, shift, nch, w.moff, w.rec1));
+    } else {
     TIMED("hist_l1", hipLaunchKernelGGL(k_hist_l1<Src>, dim3(q.nch1), dim3(L1_THREADS), lds_hist_l1(P, window), st, P,
                                         src, nkmers, q.ck1, q.nch1, w.mcnt));
     TIMED("scan", scan_counts(g, w.mcnt, w.moff, F1 * q.nch1));
     TIMED("plan_l2", hipLaunchKernelGGL(k_plan_l2, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1, q.nch1,
                                         w.moff, w.mcnt, w.off1, w.ch2));
-    // records this pass writes (all of them on one device; the owned ones on a shard)
-    uint64_t nrec = 0;
     KH_HIP(hipMemcpyAsync(&nrec, w.off1 + F1, 8, hipMemcpyDeviceToHost, st));
     KH_HIP(hipStreamSynchronize(st));
     ensure_recs(g, nrec);
@@ -351,6 +428,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
         TIMED("scatter_l1", hipLaunchKernelGGL(l1_kernel<Src>(l1_seg(P) != 0, kpt), dim3(q.nch1), dim3(L1_THREADS),
                                                lds_scatter_l1(P, window, tile_kmers), st, P, src, nkmers, q.ck1,
                                                q.nch1, t0, nt, w.moff, w.rec1));
+    }
     }
     if (check_mode()) check_holes(g, w.rec1, nrec, "scatter_l1");
     // level 2
@@ -783,9 +861,18 @@ void graph_prepare_params(Graph *g) {
     const char *ab = getenv("KH_ABLATE");
     P.ablate = ab ? atoi(ab) : 0;
     P.s0 = g->kind == BIT ? 14 : 13;
-    uint64_t maxreg = 1;
-    for (int i = 0; i < g->n; i++) maxreg = std::max<uint64_t>(maxreg, (g->lsz[i] + (1ull << P.s0) - 1) >> P.s0);
-    P.s2 = std::min(10, ceil_log2(maxreg));
+    // regions per level-1 bucket: about sqrt(total regions), so both levels
+    // fan out to a few hundred destinations (few same-address LDS atomics in
+    // the tile ranks), at most 1024 (C2 on one device: 477 x 1024; a shard of
+    // an 8-way group: 240 x 256 instead of 60 x 1024)
+    uint64_t maxreg = 1, nreg = 0;
+    for (int i = 0; i < g->n; i++) {
+        const uint64_t r = (g->lsz[i] + (1ull << P.s0) - 1) >> P.s0;
+        maxreg = std::max<uint64_t>(maxreg, r);
+        nreg += r;
+    }
+    const int half = (ceil_log2(std::max<uint64_t>(nreg, 1)) + 1) / 2;
+    P.s2 = std::min({10, ceil_log2(maxreg), std::max(half, 1)});
     const uint64_t span = 1ull << (P.s0 + P.s2);
     uint64_t base = 0, byteoff = 0;
     for (int i = 0; i < g->n; i++) {
@@ -822,6 +909,19 @@ static void set_lds_limits() {
             KH_LDS_MAX(l1_kernel<SrcHashes>(seg, kpt));
         }
     KH_LDS_MAX((k_scatter_l2<PT_THREADS, L2_SEG, L2_RPT>));
+    KH_LDS_MAX((k_scatter_rec<PT_THREADS, L2_SEG, L2_RPT>));
+    KH_LDS_MAX((k_own_filter<SrcTwoBit, 1>));
+    KH_LDS_MAX((k_own_filter<SrcTwoBit, 2>));
+    KH_LDS_MAX((k_own_filter<SrcTwoBit, 4>));
+    KH_LDS_MAX((k_own_filter<SrcTwoBit, 8>));
+    KH_LDS_MAX((k_own_filter<SrcBytes, 1>));
+    KH_LDS_MAX((k_own_filter<SrcBytes, 2>));
+    KH_LDS_MAX((k_own_filter<SrcBytes, 4>));
+    KH_LDS_MAX((k_own_filter<SrcBytes, 8>));
+    KH_LDS_MAX((k_own_filter<SrcHashes, 1>));
+    KH_LDS_MAX((k_own_filter<SrcHashes, 2>));
+    KH_LDS_MAX((k_own_filter<SrcHashes, 4>));
+    KH_LDS_MAX((k_own_filter<SrcHashes, 8>));
     KH_LDS_MAX((k_scatter_w<PT_THREADS, 8>));
 #undef KH_LDS_MAX
     (void)hipFuncSetAttribute((const void *)k_mark, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
@@ -885,7 +985,7 @@ Graph::~Graph() {
     Workspace &w = ws;
     void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.fullf, w.newbits, w.bc, w.off1, w.ch2,
                     w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.cross, w.ctr, w.d_words, w.d_koff, w.d_bytes,
-                    w.q_hashes, w.q_counts};
+                    w.q_hashes, w.q_counts, w.frec, w.fcount};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (w.h_ctr) (void)hipHostFree(w.h_ctr);

@@ -72,6 +72,9 @@ struct Params {
 struct Workspace {
     uint64_t cap_kmers = 0, cap_recs = 0;
     uint64_t *rec1 = nullptr, *rec2 = nullptr;   // (k-mer index << 32) | bin offset
+    uint64_t *frec = nullptr;                    // a shard's owned records (k_own_filter)
+    uint64_t cap_frec = 0;
+    unsigned long long *fcount = nullptr;        // k_own_filter output counter
     uint8_t *fullf = nullptr;                    // per k-mer bigcount "full" tallies
     uint32_t *newbits = nullptr;                 // per k-mer new flags (bitmap)
     uint64_t *bc = nullptr;                      // bigcount candidate hashes

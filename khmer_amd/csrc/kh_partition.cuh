@@ -419,6 +419,197 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
 }
 
 // ---------------------------------------------------------------------------
+// Level 1 of a shard ("owned filter").  A shard of a G-rank group owns ~1/G
+// of every table's bins but hashes every k-mer of the stream, so with
+// k_hist_l1 + k_scatter_l1 it would hash each k-mer twice and run the whole
+// tile machinery of scatter_l1 for ~1/G useful records.  k_own_filter hashes
+// every k-mer once and keeps only the owned records, (j << 32) | G with the
+// local bin id G < 2^32.  They collect in an LDS buffer of OWN_BUF records
+// (tile-wide scan for the slots) that is flushed as one contiguous run, so
+// one returning global atomic reserves output space per ~OWN_BUF records (a
+// per-tile atomic on the single counter serialised at ~12 ns each).  Records
+// past `cap` are counted but not written; the host then re-runs the filter
+// into a larger buffer.  k_hist_rec / k_scatter_rec bucket the record stream
+// the way level 2 buckets its input, into the same bucket-major level-1
+// layout k_scatter_l1 writes, so everything after level 1 is unchanged.
+constexpr int OWN_BUF = 8192;
+template <class Src, int KPT>
+__global__ void __launch_bounds__(L1_THREADS) k_own_filter(Params P, Src src, uint64_t nkmers, uint32_t ck, int t0,
+                                                          int nt, uint64_t cap, uint64_t *out,
+                                                          unsigned long long *count) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *buf = (uint64_t *)smem;                     // [OWN_BUF]
+    uint32_t *s_wtot = (uint32_t *)(buf + OWN_BUF);       // [16]
+    unsigned long long *s_base = (unsigned long long *)(s_wtot + 16);
+    uint64_t *s_meta = (uint64_t *)(s_base + 1);
+    uint64_t *s_koff = s_meta + 2;
+    constexpr int TILE_KMERS = L1_THREADS * KPT;
+    static_assert(TILE_KMERS * (L1_MAX_RPT / KPT) <= OWN_BUF, "a tile must fit the buffer");
+    const uint64_t c0 = (uint64_t)blockIdx.x * ck;
+    const uint64_t c1 = min(nkmers, c0 + ck);
+    const bool pre = !needs_window(src);
+    typename Src::Pend pend[KPT];
+    if (pre) {
+#pragma unroll
+        for (int a = 0; a < KPT; a++) {
+            const uint64_t j = c0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            if (j < min(c1, c0 + TILE_KMERS)) pend[a] = kmer_fetch(src, j);
+        }
+    }
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nwaves = blockDim.x >> 6;
+    // buffered records -> out (all threads; nb block-uniform)
+    auto flush = [&](uint32_t nb) {
+        if (threadIdx.x == 0) *s_base = atomicAdd(count, (unsigned long long)nb);
+        block_sync();
+        const uint64_t base = *s_base;
+        for (uint32_t x = threadIdx.x; x < nb; x += blockDim.x)
+            if (base + x < cap) out[base + x] = buf[x];
+        block_sync();
+    };
+    uint32_t nb = 0;   // records in buf
+    const uint32_t ntiles = uniform_u32((uint32_t)((c1 - c0 + TILE_KMERS - 1) / TILE_KMERS));
+    for (uint32_t ti = 0; ti < ntiles; ti++) {
+        const uint64_t j0 = c0 + (uint64_t)ti * TILE_KMERS;
+        const uint64_t j1 = min(c1, j0 + TILE_KMERS);
+        block_sync();
+        TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
+        uint64_t v[L1_MAX_RPT];
+        uint32_t own = 0;   // bit q: record slot q is owned here
+        uint64_t hh[KPT];
+#pragma unroll
+        for (int a = 0; a < KPT; a++) {
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            hh[a] = j < j1 ? (pre ? src.finish(pend[a]) : kmer_hash(src, s_koff, tr, j)) : 0;
+        }
+        if (pre) {
+            const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
+#pragma unroll
+            for (int a = 0; a < KPT; a++) {
+                const uint64_t j = n0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+                if (j < n1) pend[a] = kmer_fetch(src, j);
+            }
+        }
+        constexpr int TPK = L1_MAX_RPT / KPT;   // table slots per k-mer
+#pragma unroll
+        for (int a = 0; a < KPT; a++) {
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+#pragma unroll
+            for (int i = 0; i < TPK; i++) {
+                uint64_t G;
+                if (i < nt && j < j1 && local_bin(P, t0 + i, hh[a], &G)) {
+                    v[a * TPK + i] = (j << 32) | G;
+                    own |= 1u << (a * TPK + i);
+                }
+            }
+        }
+        // tile-wide exclusive scan of the per-thread counts
+        const uint32_t c = __builtin_popcount(own);
+        uint32_t incl = c;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= (uint32_t)d) incl += y;
+        }
+        if (lane == 63) s_wtot[wave] = incl;
+        block_sync();
+        uint32_t tot = 0, pos = incl - c;
+        for (uint32_t w = 0; w < nwaves; w++) {
+            const uint32_t x = s_wtot[w];
+            tot += x;
+            if (w < wave) pos += x;
+        }
+        tot = uniform_u32(tot);
+        if (nb + tot > (uint32_t)OWN_BUF) {
+            flush(nb);
+            nb = 0;
+        }
+        pos += nb;
+#pragma unroll
+        for (int q = 0; q < L1_MAX_RPT; q++)
+            if ((own >> q) & 1) buf[pos + __builtin_popcount(own & ((1u << q) - 1))] = v[q];
+        nb += tot;
+    }
+    block_sync();
+    if (nb) flush(nb);
+}
+
+// per-chunk bucket histogram of a flat record stream: chunk c = records
+// [c * L2_CHUNK, ...), destination (uint32)record >> shift; M[d * nch + c]
+__global__ void __launch_bounds__(PT_THREADS) k_hist_rec(const uint64_t *rec, uint64_t n, uint32_t F, int shift,
+                                                        uint32_t nch, uint32_t *M) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *hist = (uint32_t *)smem;
+    for (uint32_t d = threadIdx.x; d < F; d += blockDim.x) hist[d] = 0;
+    block_sync();
+    const uint64_t r0 = (uint64_t)blockIdx.x * L2_CHUNK, r1 = min(n, r0 + L2_CHUNK);
+    const uint32_t *rec32 = (const uint32_t *)rec;   // low words = local bin ids
+    for (uint64_t q = r0 + threadIdx.x; q < r1; q += blockDim.x) atomicAdd(&hist[rec32[2 * q] >> shift], 1u);
+    block_sync();
+    for (uint32_t d = threadIdx.x; d < F; d += blockDim.x) M[(uint64_t)d * nch + blockIdx.x] = hist[d];
+}
+
+// register-direct bucketing of a flat record stream (k_scatter_l2's scheme):
+// record (j << 32) | G goes to bucket G >> shift as (j << 32) | (G & omask)
+template <int THREADS, int SEG, int RPT>
+__global__ void __launch_bounds__(THREADS) k_scatter_rec(const uint64_t *rec_in, uint64_t n, uint32_t F, int shift,
+                                                         uint32_t nch, const uint64_t *O, uint64_t *rec_out) {
+    constexpr int TILE = THREADS * RPT;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t Fa = (F + 3) & ~3u;
+    uint64_t *lcur = (uint64_t *)smem;               // [F]
+    uint64_t *tail = lcur + Fa;                      // [F*SEG]
+    uint32_t *hist = (uint32_t *)(tail + (size_t)Fa * SEG);  // [F]
+    uint32_t *nflush = hist + Fa;                    // [4]
+    uint16_t *flist = (uint16_t *)(nflush + 4);      // [F]
+    uint8_t *hskip = (uint8_t *)(flist + Fa);        // [F]
+    const Emit<uint64_t, SEG> em{lcur, hskip, tail, hist, nullptr, nullptr, nullptr, flist, nflush};
+    const uint64_t omask = (1ull << shift) - 1;
+    const uint64_t r0 = (uint64_t)blockIdx.x * L2_CHUNK, r1 = min(n, r0 + L2_CHUNK);
+    for (uint32_t d = threadIdx.x; d < F; d += THREADS) em.init(d, O[(uint64_t)d * nch + blockIdx.x]);
+    if (threadIdx.x == 0) *nflush = 0;
+    uint64_t v[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; q++) {
+        const uint64_t idx = r0 + (uint64_t)q * THREADS + threadIdx.x;
+        v[q] = idx < min(r1, r0 + TILE) ? rec_in[idx] : ~0ull;
+    }
+    const uint32_t ntiles = uniform_u32((uint32_t)((r1 - r0 + TILE - 1) / TILE));
+    for (uint32_t ti = 0; ti < ntiles; ti++) {
+        const uint64_t t0 = r0 + (uint64_t)ti * TILE;
+        const bool last = ti + 1 == ntiles;
+        block_sync();
+        uint32_t rank[RPT];
+        uint64_t x[RPT];
+#pragma unroll
+        for (int q = 0; q < RPT; q++) {
+            x[q] = v[q];
+            if (x[q] != ~0ull) {
+                rank[q] = atomicAdd(&hist[(uint32_t)x[q] >> shift], 1u);
+                em.note((uint32_t)x[q] >> shift, rank[q], last);
+            }
+        }
+        {
+            const uint64_t n0 = t0 + TILE, n1 = min(r1, n0 + TILE);
+#pragma unroll
+            for (int q = 0; q < RPT; q++) {
+                const uint64_t idx = n0 + (uint64_t)q * THREADS + threadIdx.x;
+                v[q] = idx < n1 ? rec_in[idx] : ~0ull;
+            }
+        }
+        block_sync();
+        em.flush_listed(F, last, rec_out);
+        block_sync();
+#pragma unroll
+        for (int q = 0; q < RPT; q++)
+            if (x[q] != ~0ull)
+                em.put_rank((uint32_t)x[q] >> shift, rank[q], (x[q] & ~0xFFFFFFFFull) | (x[q] & omask), last,
+                            rec_out);
+        block_sync();
+        em.advance(F, last);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // level 2: chunk t of the level-1 output lies in bucket b (ch2[b] <= t < ch2[b+1])
 struct L2Chunk {
     uint32_t b, c, nc;
