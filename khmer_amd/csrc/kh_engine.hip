@@ -313,7 +313,7 @@ template <class Src, int KPT>
 static void launch_own_filter(Graph *g, const Src &src, uint64_t nkmers, bool window, int t0, int nt) {
     constexpr uint32_t CK = 32768;
     const uint32_t nch = (uint32_t)((nkmers + CK - 1) / CK);
-    const size_t lds = (size_t)OWN_BUF * 8 + 16 * 4 + 8 + lds_window(window, L1_THREADS * KPT);
+    const size_t lds = (size_t)OWN_BUF * 8 + 32 * 4 + 8 + lds_window(window, L1_THREADS * KPT);
     hipLaunchKernelGGL((k_own_filter<Src, KPT>), dim3(nch), dim3(L1_THREADS), lds, g->stream, g->prm, src, nkmers,
                        CK, t0, nt, g->ws.cap_frec, g->ws.frec, g->ws.fcount);
 }
@@ -330,11 +330,12 @@ static uint64_t own_filter(Graph *g, const Src &src, uint64_t nkmers, bool windo
     if (!w.fcount) KH_HIP(hipMalloc((void **)&w.fcount, 64));
     for (int attempt = 0;; attempt++) {
         KH_HIP(hipMemsetAsync(w.fcount, 0, 8, g->stream));
-        for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
-            const int nt = std::min(L1_MAX_RPT, P.n - t0);
+        for (int t0 = 0; t0 < P.n; t0 += OWN_RPT) {
+            const int nt = std::min(OWN_RPT, P.n - t0);
             int kpt = 1;
-            while (kpt * 2 * nt <= L1_MAX_RPT) kpt *= 2;
+            while (kpt * 2 * nt <= OWN_RPT) kpt *= 2;
             TIMED("own_filter", switch (kpt) {
+                case 16: launch_own_filter<Src, 16>(g, src, nkmers, window, t0, nt); break;
                 case 8: launch_own_filter<Src, 8>(g, src, nkmers, window, t0, nt); break;
                 case 4: launch_own_filter<Src, 4>(g, src, nkmers, window, t0, nt); break;
                 case 2: launch_own_filter<Src, 2>(g, src, nkmers, window, t0, nt); break;
@@ -914,14 +915,17 @@ static void set_lds_limits() {
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 2>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 4>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 8>));
+    KH_LDS_MAX((k_own_filter<SrcTwoBit, 16>));
     KH_LDS_MAX((k_own_filter<SrcBytes, 1>));
     KH_LDS_MAX((k_own_filter<SrcBytes, 2>));
     KH_LDS_MAX((k_own_filter<SrcBytes, 4>));
     KH_LDS_MAX((k_own_filter<SrcBytes, 8>));
+    KH_LDS_MAX((k_own_filter<SrcBytes, 16>));
     KH_LDS_MAX((k_own_filter<SrcHashes, 1>));
     KH_LDS_MAX((k_own_filter<SrcHashes, 2>));
     KH_LDS_MAX((k_own_filter<SrcHashes, 4>));
     KH_LDS_MAX((k_own_filter<SrcHashes, 8>));
+    KH_LDS_MAX((k_own_filter<SrcHashes, 16>));
     KH_LDS_MAX((k_scatter_w<PT_THREADS, 8>));
 #undef KH_LDS_MAX
     (void)hipFuncSetAttribute((const void *)k_mark, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
@@ -1029,6 +1033,7 @@ struct ShardGroup {
     int world = 1, rank0 = 0, nlocal = 1;
     std::vector<Graph *> shards;
     ncclComm_t comm = nullptr;
+    ncclComm_t comm_b = nullptr;     // source-read broadcasts (own stream, overlapped with compute)
     struct Local {
         uint64_t *src = nullptr;
         uint64_t cap_src = 0;        // broadcast reads of another rank (RCCL)
@@ -1044,6 +1049,14 @@ struct ShardGroup {
         uint64_t cap_flist = 0;      // own full-tally list
         uint64_t *fall = nullptr;
         uint64_t cap_fall = 0;       // gathered full-tally lists
+        // source reads in flight: two slots filled on the transfer stream
+        // (RCCL broadcast on comm_b; a device copy in loopback) while the
+        // compute stream consumes the other one
+        uint64_t *slot[2] = {nullptr, nullptr};
+        uint64_t cap_slot[2] = {0, 0};
+        hipStream_t st_x = nullptr;
+        hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
+        bool freed[2] = {false, false};
     };
     std::vector<Local> loc;
     uint64_t *d_red = nullptr;
@@ -1051,11 +1064,19 @@ struct ShardGroup {
     ~ShardGroup() {
         for (size_t l = 0; l < loc.size(); l++) {
             (void)hipSetDevice(shards[l]->device);
-            for (void *p : {(void *)loc[l].src, (void *)loc[l].recv, (void *)loc[l].ws, (void *)loc[l].ws_all,
-                            (void *)loc[l].roff, (void *)loc[l].flist, (void *)loc[l].fall})
+            auto &lc = loc[l];
+            if (lc.st_x) (void)hipStreamSynchronize(lc.st_x);
+            for (void *p : {(void *)lc.src, (void *)lc.recv, (void *)lc.ws, (void *)lc.ws_all, (void *)lc.roff,
+                            (void *)lc.flist, (void *)lc.fall, (void *)lc.slot[0], (void *)lc.slot[1]})
                 if (p) (void)hipFree(p);
+            for (int b = 0; b < 2; b++) {
+                if (lc.ev_ready[b]) (void)hipEventDestroy(lc.ev_ready[b]);
+                if (lc.ev_free[b]) (void)hipEventDestroy(lc.ev_free[b]);
+            }
+            if (lc.st_x) (void)hipStreamDestroy(lc.st_x);
         }
         if (d_red) (void)hipFree(d_red);
+        if (comm_b) (void)ncclCommDestroy(comm_b);
         if (comm) (void)ncclCommDestroy(comm);
         for (Graph *g : shards) delete g;
     }
@@ -1088,6 +1109,7 @@ ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n
         memcpy(&id, uid, sizeof id);
         KH_HIP(hipSetDevice(devices[0]));
         KH_NCCL(ncclCommInitRank(&G->comm, world, id, rank));
+        KH_NCCL(ncclCommSplit(G->comm, 0, rank, &G->comm_b, nullptr));
         KH_HIP(hipMalloc((void **)&G->d_red, 256 * 8));   // [0,64) gathers, [128,..) scalars
     }
     return G.release();
@@ -1271,23 +1293,54 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
     const uint64_t rpb0 = std::max<uint64_t>(1, std::min<uint64_t>(g0->batch_kmers, MAX_PASS_KMERS) / kpr);
     const uint64_t npass = std::max<uint64_t>(1, (nreads + rpb0 - 1) / rpb0);
     const uint64_t rpb = std::max<uint64_t>(1, (nreads + npass - 1) / npass);   // equal passes
-    for (int s = 0; s < W; s++) {
-        std::vector<const uint64_t *> buf(NL);
-        if (G->comm) {
-            auto &lc = G->loc[0];
-            KH_HIP(hipSetDevice(g0->device));
-            uint64_t *dst;
-            if (G->rank0 == s) {
-                dst = const_cast<uint64_t *>(d_words[0]);
-            } else {
-                ensure((void **)&lc.src, &lc.cap_src, nwords, 8);
-                dst = lc.src;
+    // Source s's reads travel into slot s & 1 on the transfer stream while the
+    // compute stream consumes source s - 1 from the other slot: events order
+    // slot reuse (ev_free, recorded after a source's last pass) and use
+    // (ev_ready).  RCCL: a broadcast on comm_b, the root in place on its own
+    // buffer.  Loopback: a device copy (the same schedule without RCCL).
+    for (int l = 0; l < NL; l++) {
+        auto &lc = G->loc[l];
+        KH_HIP(hipSetDevice(G->shards[l]->device));
+        if (!lc.st_x) {
+            KH_HIP(hipStreamCreateWithFlags(&lc.st_x, hipStreamNonBlocking));
+            for (int b = 0; b < 2; b++) {
+                KH_HIP(hipEventCreateWithFlags(&lc.ev_ready[b], hipEventDisableTiming));
+                KH_HIP(hipEventCreateWithFlags(&lc.ev_free[b], hipEventDisableTiming));
             }
-            Graph *g = g0;
-            TIMED("bcast", KH_NCCL(ncclBroadcast(dst, dst, nwords, ncclUint64, s, G->comm, g->stream)));
-            buf[0] = dst;
-        } else {
-            for (int l = 0; l < NL; l++) buf[l] = d_words[s];
+        }
+        for (int b = 0; b < 2; b++) lc.freed[b] = false;   // each slot's last reader is done (synchronised)
+    }
+    const bool rccl = G->comm != nullptr;
+    auto own = [&](int s, int l) { return rccl && G->rank0 + l == s; };
+    auto transfer = [&](int s) {
+        for (int l = 0; l < NL; l++) {
+            auto &lc = G->loc[l];
+            const int b = s & 1;
+            KH_HIP(hipSetDevice(G->shards[l]->device));
+            if (lc.freed[b]) KH_HIP(hipStreamWaitEvent(lc.st_x, lc.ev_free[b], 0));
+            if (own(s, l)) {
+                uint64_t *w = const_cast<uint64_t *>(d_words[0]);
+                KH_NCCL(ncclBroadcast(w, w, nwords, ncclUint64, s, G->comm_b, lc.st_x));
+            } else {
+                if (lc.cap_slot[b] < nwords) KH_HIP(hipStreamSynchronize(lc.st_x));   // slot about to be reallocated
+                ensure((void **)&lc.slot[b], &lc.cap_slot[b], nwords, 8);
+                if (rccl)
+                    KH_NCCL(ncclBroadcast(lc.slot[b], lc.slot[b], nwords, ncclUint64, s, G->comm_b, lc.st_x));
+                else
+                    KH_HIP(hipMemcpyAsync(lc.slot[b], d_words[s], nwords * 8, hipMemcpyDeviceToDevice, lc.st_x));
+            }
+            KH_HIP(hipEventRecord(lc.ev_ready[b], lc.st_x));
+        }
+    };
+    transfer(0);
+    for (int s = 0; s < W; s++) {
+        if (s + 1 < W) transfer(s + 1);
+        std::vector<const uint64_t *> buf(NL);
+        for (int l = 0; l < NL; l++) {
+            auto &lc = G->loc[l];
+            KH_HIP(hipSetDevice(G->shards[l]->device));
+            KH_HIP(hipStreamWaitEvent(G->shards[l]->stream, lc.ev_ready[s & 1], 0));
+            buf[l] = own(s, l) ? d_words[0] : lc.slot[s & 1];
         }
         for (uint64_t r0 = 0; r0 < nreads; r0 += rpb) {
             const uint64_t nr = std::min(rpb, nreads - r0);
@@ -1312,6 +1365,17 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
                 pass_stage_c(G->shards[l], srcs[l], ps[l], nullptr);
             }
         }
+        for (int l = 0; l < NL; l++) {
+            auto &lc = G->loc[l];
+            KH_HIP(hipSetDevice(G->shards[l]->device));
+            KH_HIP(hipEventRecord(lc.ev_free[s & 1], G->shards[l]->stream));
+            lc.freed[s & 1] = true;
+        }
+    }
+    for (int l = 0; l < NL; l++) {
+        KH_HIP(hipSetDevice(G->shards[l]->device));
+        KH_HIP(hipStreamSynchronize(G->loc[l].st_x));
+        KH_HIP(hipStreamSynchronize(G->shards[l]->stream));   // the slots are free for the next call
     }
 }
 

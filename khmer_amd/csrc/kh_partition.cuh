@@ -433,18 +433,20 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
 // the way level 2 buckets its input, into the same bucket-major level-1
 // layout k_scatter_l1 writes, so everything after level 1 is unchanged.
 constexpr int OWN_BUF = 8192;
+constexpr int OWN_RPT = 16;   // record slots per thread per tile
 template <class Src, int KPT>
 __global__ void __launch_bounds__(L1_THREADS) k_own_filter(Params P, Src src, uint64_t nkmers, uint32_t ck, int t0,
                                                           int nt, uint64_t cap, uint64_t *out,
                                                           unsigned long long *count) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t *buf = (uint64_t *)smem;                     // [OWN_BUF]
-    uint32_t *s_wtot = (uint32_t *)(buf + OWN_BUF);       // [16]
-    unsigned long long *s_base = (unsigned long long *)(s_wtot + 16);
+    uint32_t *s_wtot = (uint32_t *)(buf + OWN_BUF);       // [2][16] (tile parity)
+    unsigned long long *s_base = (unsigned long long *)(s_wtot + 32);
     uint64_t *s_meta = (uint64_t *)(s_base + 1);
     uint64_t *s_koff = s_meta + 2;
     constexpr int TILE_KMERS = L1_THREADS * KPT;
-    static_assert(TILE_KMERS * (L1_MAX_RPT / KPT) <= OWN_BUF, "a tile must fit the buffer");
+    constexpr int TPK = OWN_RPT / KPT;   // table slots per k-mer
+    static_assert(L1_THREADS * OWN_RPT <= OWN_BUF, "a tile must fit the buffer");
     const uint64_t c0 = (uint64_t)blockIdx.x * ck;
     const uint64_t c1 = min(nkmers, c0 + ck);
     const bool pre = !needs_window(src);
@@ -472,9 +474,11 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_filter(Params P, Src src, ui
     for (uint32_t ti = 0; ti < ntiles; ti++) {
         const uint64_t j0 = c0 + (uint64_t)ti * TILE_KMERS;
         const uint64_t j1 = min(c1, j0 + TILE_KMERS);
-        block_sync();
+        // (no barrier needed here on the fixed-length path: the per-tile
+        // wave totals alternate between two slots, and buf is only read by
+        // flush(), which synchronises around its reads)
         TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
-        uint64_t v[L1_MAX_RPT];
+        uint64_t v[OWN_RPT];
         uint32_t own = 0;   // bit q: record slot q is owned here
         uint64_t hh[KPT];
 #pragma unroll
@@ -490,7 +494,6 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_filter(Params P, Src src, ui
                 if (j < n1) pend[a] = kmer_fetch(src, j);
             }
         }
-        constexpr int TPK = L1_MAX_RPT / KPT;   // table slots per k-mer
 #pragma unroll
         for (int a = 0; a < KPT; a++) {
             const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
@@ -504,17 +507,18 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_filter(Params P, Src src, ui
             }
         }
         // tile-wide exclusive scan of the per-thread counts
+        uint32_t *wt = s_wtot + (ti & 1) * 16;
         const uint32_t c = __builtin_popcount(own);
         uint32_t incl = c;
         for (int d = 1; d < 64; d <<= 1) {
             const uint32_t y = __shfl_up(incl, d, 64);
             if (lane >= (uint32_t)d) incl += y;
         }
-        if (lane == 63) s_wtot[wave] = incl;
+        if (lane == 63) wt[wave] = incl;
         block_sync();
         uint32_t tot = 0, pos = incl - c;
         for (uint32_t w = 0; w < nwaves; w++) {
-            const uint32_t x = s_wtot[w];
+            const uint32_t x = wt[w];
             tot += x;
             if (w < wave) pos += x;
         }
@@ -525,7 +529,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_filter(Params P, Src src, ui
         }
         pos += nb;
 #pragma unroll
-        for (int q = 0; q < L1_MAX_RPT; q++)
+        for (int q = 0; q < OWN_RPT; q++)
             if ((own >> q) & 1) buf[pos + __builtin_popcount(own & ((1u << q) - 1))] = v[q];
         nb += tot;
     }
