@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include <rocprim/device/device_scan.hpp>
@@ -258,10 +259,10 @@ using L1Fn = void (*)(Params, Src, uint64_t, uint32_t, uint32_t, int, int, uint6
 template <class Src>
 static L1Fn<Src> l1_kernel(bool seg, int kpt) {
     switch (kpt) {
-        case 8: return seg ? k_scatter_l1<Src, 8, 8> : k_scatter_l1<Src, 0, 8>;
-        case 4: return seg ? k_scatter_l1<Src, 8, 4> : k_scatter_l1<Src, 0, 4>;
-        case 2: return seg ? k_scatter_l1<Src, 8, 2> : k_scatter_l1<Src, 0, 2>;
-        default: return seg ? k_scatter_l1<Src, 8, 1> : k_scatter_l1<Src, 0, 1>;
+        case 8: return seg ? k_scatter_l1<Src, 2, 8> : k_scatter_l1<Src, 0, 8>;
+        case 4: return seg ? k_scatter_l1<Src, 2, 4> : k_scatter_l1<Src, 0, 4>;
+        case 2: return seg ? k_scatter_l1<Src, 2, 2> : k_scatter_l1<Src, 0, 2>;
+        default: return seg ? k_scatter_l1<Src, 2, 1> : k_scatter_l1<Src, 0, 1>;
     }
 }
 
@@ -271,22 +272,52 @@ static size_t lds_window(bool window, int tile_kmers) { return 16 + (window ? (s
 static size_t lds_hist_l1(const Params &P, bool window) {
     return (size_t)((P.F1 + 3) & ~3u) * 4 + lds_window(window, L1_HIST_TILE);
 }
-// level-1 tail buffers (64 B per bucket) when they fit next to the tile
-static int l1_seg(const Params &P) { return P.F1 <= 1024 ? 8 : 0; }
+// level-1 tails of 2 records (16-B aligned runs) when they fit next to the
+// tile.  Measured on C2 (scatter_l1 ms/step): no tails 128, 2 records 108,
+// 4 records 114, 8 records 122 -- every tile flushes nearly every bucket's
+// tail, so smaller tails mean fewer LDS slot scans per tile.
+static int l1_seg(const Params &P) { return P.F1 <= 1024 ? 2 : 0; }
 static size_t lds_scatter_l1(const Params &P, bool window, int tile_kmers) {
     const size_t F1a = (P.F1 + 3) & ~3u;
-    return F1a * 8 + (size_t)L1_TILE_RECS * 8 + F1a * 8 * l1_seg(P) + F1a * 4 * 2 +
-           (size_t)L1_TILE_RECS * 2 + 64 + ((F1a + 7) & ~7u) + lds_window(window, tile_kmers);
+    const int seg = l1_seg(P);
+    const size_t tile = (size_t)L1_THREADS * L1_MAX_RPT;
+    return F1a * 8 + tile * 8 + F1a * 8 * seg + F1a * 4 * 2 + tile * 2 + 64 + ((F1a + 7) & ~7u) +
+           lds_window(window, tile_kmers);
 }
+
 constexpr int L2_SEG = 16;   // 128-B level-2 write segments
 constexpr int L2_RPT = 8;    // level-2 records per thread per tile
+static int env_seg(const char *name, int dflt) {   // development: KH_L2_SEG / KH_W_SEG tail sizes
+    const char *e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+static int l2_seg() { return env_seg("KH_L2_SEG", L2_SEG); }
+static int w_seg() { return env_seg("KH_W_SEG", 2); }   // measured: 8 -> 26.8, 2 -> 25.5 ms/step
 static size_t lds_scatter_l2(const Params &P) {
     const size_t F2 = (size_t)1 << P.s2;
-    return F2 * 8 + F2 * 8 * L2_SEG + F2 * 4 + 8 + ((F2 + 1) & ~(size_t)1) * 2 + F2;
+    return F2 * 8 + F2 * 8 * l2_seg() + F2 * 4 + 8 + ((F2 + 1) & ~(size_t)1) * 2 + F2;
+}
+using L2Fn = void (*)(uint32_t, int, int, const uint64_t *, const uint32_t *, const uint64_t *, const uint64_t *,
+                      uint64_t *);
+static L2Fn l2_kernel() {
+    switch (l2_seg()) {
+        case 2: return k_scatter_l2<PT_THREADS, 2, L2_RPT>;
+        case 4: return k_scatter_l2<PT_THREADS, 4, L2_RPT>;
+        case 8: return k_scatter_l2<PT_THREADS, 8, L2_RPT>;
+        default: return k_scatter_l2<PT_THREADS, 16, L2_RPT>;
+    }
+}
+using WFn = void (*)(Params, ApplyArgs, int, uint32_t, uint32_t, const uint64_t *, uint32_t *);
+static WFn w_kernel() {
+    switch (w_seg()) {
+        case 2: return k_scatter_w<PT_THREADS, 2>;
+        case 4: return k_scatter_w<PT_THREADS, 4>;
+        default: return k_scatter_w<PT_THREADS, 8>;
+    }
 }
 static size_t lds_scatter_w(uint32_t FJ) {
     const size_t FJa = (FJ + 3) & ~3u;
-    return W_RPC * 8 + (W_RPC + 4) * 4 + FJa * 8 + (size_t)PT_TILE * 4 + FJa * 32 + FJa * 4 * 2 + 64 + FJa;
+    return W_RPC * 8 + (W_RPC + 4) * 4 + FJa * 8 + (size_t)PT_TILE * 4 + FJa * 4 * w_seg() + FJa * 4 * 2 + 64 + FJa;
 }
 static size_t lds_apply(const Params &P) {
     const size_t R = (size_t)1 << P.s0;
@@ -297,17 +328,11 @@ static size_t lds_apply(const Params &P) {
 // small share of the bins: a group of >= KH_OWN_FILTER_MIN ranks (default 3;
 // 0 disables), local bin ids below 2^32 and at most 1024 level-1 buckets.
 static bool use_own_filter(const Graph *g) {
-    static const int min_world = [] {
-        const char *e = getenv("KH_OWN_FILTER_MIN");
-        return e && *e ? atoi(e) : 3;
-    }();
+    const char *e = getenv("KH_OWN_FILTER_MIN");
+    const int min_world = e && *e ? atoi(e) : 3;
     const Params &P = g->prm;
     return min_world > 0 && g->world >= min_world && P.F1 <= 1024 &&
            ((uint64_t)P.F1 << (P.s0 + P.s2)) <= (1ull << 32);
-}
-static size_t lds_scatter_rec(uint64_t F) {
-    const size_t Fa = (F + 3) & ~3ull;
-    return Fa * 8 + Fa * 8 * L2_SEG + Fa * 4 + 16 + Fa * 2 + Fa;
 }
 template <class Src, int KPT>
 static void launch_own_filter(Graph *g, const Src &src, uint64_t nkmers, bool window, int t0, int nt) {
@@ -325,7 +350,11 @@ static uint64_t own_filter(Graph *g, const Src &src, uint64_t nkmers, bool windo
     Workspace &w = g->ws;
     double expect = 0;
     for (int i = 0; i < P.n; i++) expect += (double)nkmers * (double)P.lsz[i] / (double)P.p[i];
-    const uint64_t want = (uint64_t)(expect * 1.05) + (1u << 20);
+    // first buffer: the expectation + 5 % (KH_OWN_FILTER_FRAC overrides the
+    // factor; below 1 it forces the re-run path, for tests)
+    const char *fe = getenv("KH_OWN_FILTER_FRAC");
+    const double frac = fe && *fe ? atof(fe) : 1.05;
+    const uint64_t want = (uint64_t)(expect * frac) + (frac < 1 ? 0 : (1u << 20));
     ensure((void **)&w.frec, &w.cap_frec, want, 8);
     if (!w.fcount) KH_HIP(hipMalloc((void **)&w.fcount, 64));
     for (int attempt = 0;; attempt++) {
@@ -406,9 +435,13 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
             KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
             KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
         }
-        TIMED("scatter_rec", hipLaunchKernelGGL((k_scatter_rec<PT_THREADS, L2_SEG, L2_RPT>), dim3(nch),
-                                                dim3(PT_THREADS), lds_scatter_rec(F1), st, w.frec, nrec,
-                                                (uint32_t)F1, shift, nch, w.moff, w.rec1));
+        SrcHashes rs{};
+        rs.h = w.frec;
+        rs.k = P.k;
+        TIMED("scatter_l1", hipLaunchKernelGGL((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>),
+                                               dim3(nch), dim3(L1_THREADS),
+                                               lds_scatter_l1(P, false, L1_THREADS * L1_MAX_RPT), st, P, rs, nrec,
+                                               (uint32_t)L2_CHUNK, nch, 0, 1, w.moff, w.rec1));
     } else {
     TIMED("hist_l1", hipLaunchKernelGGL(k_hist_l1<Src>, dim3(q.nch1), dim3(L1_THREADS), lds_hist_l1(P, window), st, P,
                                         src, nkmers, q.ck1, q.nch1, w.mcnt));
@@ -439,7 +472,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     TIMED("scan", scan_counts(g, w.mcnt, w.moff, F2 * q.nch2max));
     TIMED("off2", hipLaunchKernelGGL(k_off2, dim3((unsigned)std::min<uint64_t>((F1 * F2 + 255) / 256, 8192)),
                                      dim3(256), 0, st, (uint32_t)F1, P.s2, w.off1, w.ch2, w.moff, w.off2));
-    TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2<PT_THREADS, L2_SEG, L2_RPT>), dim3(g2), dim3(PT_THREADS),
+    TIMED("scatter_l2", hipLaunchKernelGGL(l2_kernel(), dim3(g2), dim3(PT_THREADS),
                                            lds_scatter_l2(P), st, (uint32_t)F1, P.s0, P.s2, w.off1, w.ch2, w.moff,
                                            w.rec1, w.rec2));
 
@@ -480,7 +513,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     TIMED("hist_w", hipLaunchKernelGGL(k_hist_w, dim3(q.nchw), dim3(PT_THREADS), wmeta + (size_t)q.FJ * 4, st, P, A,
                                        q.js, q.FJ, q.nchw, w.mcnt));
     TIMED("scan", scan_counts(g, w.mcnt, w.moff, (uint64_t)q.FJ * q.nchw));
-    TIMED("scatter_w", hipLaunchKernelGGL((k_scatter_w<PT_THREADS, 8>), dim3(q.nchw), dim3(PT_THREADS),
+    TIMED("scatter_w", hipLaunchKernelGGL(w_kernel(), dim3(q.nchw), dim3(PT_THREADS),
                                           lds_scatter_w(q.FJ), st, P, A, q.js, q.FJ, q.nchw, w.moff, wout));
     return ps;
 }
@@ -909,8 +942,11 @@ static void set_lds_limits() {
             KH_LDS_MAX(l1_kernel<SrcBytes>(seg, kpt));
             KH_LDS_MAX(l1_kernel<SrcHashes>(seg, kpt));
         }
-    KH_LDS_MAX((k_scatter_l2<PT_THREADS, L2_SEG, L2_RPT>));
-    KH_LDS_MAX((k_scatter_rec<PT_THREADS, L2_SEG, L2_RPT>));
+    KH_LDS_MAX((k_scatter_l2<PT_THREADS, 2, L2_RPT>));
+    KH_LDS_MAX((k_scatter_l2<PT_THREADS, 4, L2_RPT>));
+    KH_LDS_MAX((k_scatter_l2<PT_THREADS, 8, L2_RPT>));
+    KH_LDS_MAX((k_scatter_l2<PT_THREADS, 16, L2_RPT>));
+    KH_LDS_MAX((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 1>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 2>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 4>));
@@ -926,6 +962,8 @@ static void set_lds_limits() {
     KH_LDS_MAX((k_own_filter<SrcHashes, 4>));
     KH_LDS_MAX((k_own_filter<SrcHashes, 8>));
     KH_LDS_MAX((k_own_filter<SrcHashes, 16>));
+    KH_LDS_MAX((k_scatter_w<PT_THREADS, 2>));
+    KH_LDS_MAX((k_scatter_w<PT_THREADS, 4>));
     KH_LDS_MAX((k_scatter_w<PT_THREADS, 8>));
 #undef KH_LDS_MAX
     (void)hipFuncSetAttribute((const void *)k_mark, hipFuncAttributeMaxDynamicSharedMemorySize, lim);

@@ -286,7 +286,10 @@ __global__ void __launch_bounds__(1024) k_plan_l2(uint32_t F1, uint32_t nch1, co
 // thread per tile, one workgroup per chunk; records stay in registers between
 // the tile histogram and the placement.  The chunk's cursors are written back
 // so a following table group continues.
-template <class Src, int SEG, int KPT>
+//
+// PRE: the source yields already-binned records (j << 32) | G (k_own_filter's
+// output; one "table", nt == 1): the same tiles, without hashing.
+template <class Src, int SEG, int KPT, int RPT = L1_MAX_RPT, bool PRE = false>
 __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, uint64_t nkmers, uint32_t ck1,
                                                           uint32_t nch1, int t0, int nt, uint64_t *O1,
                                                           uint64_t *rec) {
@@ -294,12 +297,13 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
     const uint32_t F1 = P.F1;
     const uint32_t F1a = (F1 + 3) & ~3u;
     uint64_t *lcur = (uint64_t *)smem;                // [F1]
-    uint64_t *stage = lcur + F1a;                     // [L1_TILE_RECS]
-    uint64_t *tail = stage + L1_TILE_RECS;            // [F1*SEG]
+    constexpr int TILE_RECS = L1_THREADS * RPT;
+    uint64_t *stage = lcur + F1a;                     // [TILE_RECS]
+    uint64_t *tail = stage + TILE_RECS;               // [F1*SEG]
     uint32_t *hist = (uint32_t *)(tail + (SEG > 1 ? F1a * SEG : 0));  // [F1]
     uint32_t *lstart = hist + F1a;                    // [F1]
-    uint16_t *sb = (uint16_t *)(lstart + F1a);        // [L1_TILE_RECS]
-    uint32_t *s_wtot = (uint32_t *)(sb + L1_TILE_RECS);  // [16]
+    uint16_t *sb = (uint16_t *)(lstart + F1a);        // [TILE_RECS]
+    uint32_t *s_wtot = (uint32_t *)(sb + TILE_RECS);  // [16]
     uint8_t *hskip = (uint8_t *)(s_wtot + 16);        // [F1]
     uint64_t *s_meta = (uint64_t *)(hskip + ((F1a + 7) & ~7u));
     uint64_t *s_koff = s_meta + 2;
@@ -339,12 +343,12 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
         block_sync();
         PH(0);
         TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
-        uint64_t G[L1_MAX_RPT];
-        uint32_t rank[L1_MAX_RPT];
-        uint32_t jj[L1_MAX_RPT];
+        uint64_t G[RPT];
+        uint32_t rank[RPT];
+        uint32_t jj[RPT];
         int nr = 0;
 #pragma unroll
-        for (int q = 0; q < L1_MAX_RPT; q++) { G[q] = ~0ull; rank[q] = 0; jj[q] = 0; }
+        for (int q = 0; q < RPT; q++) { G[q] = ~0ull; rank[q] = 0; jj[q] = 0; }
         // pass A: hashes, bins, tile histogram (ranks)
         uint64_t hh[KPT];
 #pragma unroll
@@ -357,13 +361,13 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
             const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
             const bool ok = j < j1;
 #pragma unroll
-            for (int q = 0; q < L1_MAX_RPT; q++) {
+            for (int q = 0; q < RPT; q++) {
                 const int i = q - a * nt;  // table slot of register q for k-mer a
                 if (ok && i >= 0 && i < nt) {
-                    uint64_t Gq;
-                    if (local_bin(P, t0 + i, hh[a], &Gq)) {   // owned here
+                    uint64_t Gq = (uint32_t)hh[a];
+                    if (PRE || local_bin(P, t0 + i, hh[a], &Gq)) {   // owned here
                         G[q] = Gq;
-                        jj[q] = (uint32_t)j;
+                        jj[q] = PRE ? (uint32_t)(hh[a] >> 32) : (uint32_t)j;
                         rank[q] = atomicAdd(&hist[(uint32_t)(Gq >> shift)], 1u);
                         nr = q + 1;
                     } else {
@@ -379,7 +383,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
         PH(2);
         // pass B: place in LDS in bucket order
 #pragma unroll
-        for (int q = 0; q < L1_MAX_RPT; q++) {
+        for (int q = 0; q < RPT; q++) {
             if (q < nr && G[q] != ~0ull) {
                 const uint32_t b = (uint32_t)(G[q] >> shift);
                 const uint32_t pos = lstart[b] + rank[q];
@@ -401,7 +405,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
         // pass C: whole segments at the chunk's cursors
         const uint32_t nrec = lstart[F1 - 1] + hist[F1 - 1];   // records staged (owned ones)
 #pragma unroll
-        for (int u = 0; u < L1_MAX_RPT; u++) {
+        for (int u = 0; u < RPT; u++) {
             const uint32_t q = threadIdx.x + (uint32_t)u * L1_THREADS;
             if (q < nrec) em.put_cur(sb[q], q, stage[q], last, rec);
         }
@@ -414,8 +418,10 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
         for (int z = 0; z < 6; z++) atomicAdd(&g_dbg[8 + z], (unsigned long long)ph[z]);
 #endif
 #undef PH
-    block_sync();
-    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) O1[(uint64_t)b * nch1 + blockIdx.x] = lcur[b];
+    if (t0 + nt < P.n) {   // a following table group continues from these cursors
+        block_sync();
+        for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) O1[(uint64_t)b * nch1 + blockIdx.x] = lcur[b];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -429,9 +435,9 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
 // one returning global atomic reserves output space per ~OWN_BUF records (a
 // per-tile atomic on the single counter serialised at ~12 ns each).  Records
 // past `cap` are counted but not written; the host then re-runs the filter
-// into a larger buffer.  k_hist_rec / k_scatter_rec bucket the record stream
-// the way level 2 buckets its input, into the same bucket-major level-1
-// layout k_scatter_l1 writes, so everything after level 1 is unchanged.
+// into a larger buffer.  k_hist_rec and k_scatter_l1<..., PRE> (the level-1
+// tiles without hashing) bucket the record stream into the same bucket-major
+// level-1 layout, so everything after level 1 is unchanged.
 constexpr int OWN_BUF = 8192;
 constexpr int OWN_RPT = 16;   // record slots per thread per tile
 template <class Src, int KPT>
@@ -550,67 +556,6 @@ __global__ void __launch_bounds__(PT_THREADS) k_hist_rec(const uint64_t *rec, ui
     for (uint64_t q = r0 + threadIdx.x; q < r1; q += blockDim.x) atomicAdd(&hist[rec32[2 * q] >> shift], 1u);
     block_sync();
     for (uint32_t d = threadIdx.x; d < F; d += blockDim.x) M[(uint64_t)d * nch + blockIdx.x] = hist[d];
-}
-
-// register-direct bucketing of a flat record stream (k_scatter_l2's scheme):
-// record (j << 32) | G goes to bucket G >> shift as (j << 32) | (G & omask)
-template <int THREADS, int SEG, int RPT>
-__global__ void __launch_bounds__(THREADS) k_scatter_rec(const uint64_t *rec_in, uint64_t n, uint32_t F, int shift,
-                                                         uint32_t nch, const uint64_t *O, uint64_t *rec_out) {
-    constexpr int TILE = THREADS * RPT;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t Fa = (F + 3) & ~3u;
-    uint64_t *lcur = (uint64_t *)smem;               // [F]
-    uint64_t *tail = lcur + Fa;                      // [F*SEG]
-    uint32_t *hist = (uint32_t *)(tail + (size_t)Fa * SEG);  // [F]
-    uint32_t *nflush = hist + Fa;                    // [4]
-    uint16_t *flist = (uint16_t *)(nflush + 4);      // [F]
-    uint8_t *hskip = (uint8_t *)(flist + Fa);        // [F]
-    const Emit<uint64_t, SEG> em{lcur, hskip, tail, hist, nullptr, nullptr, nullptr, flist, nflush};
-    const uint64_t omask = (1ull << shift) - 1;
-    const uint64_t r0 = (uint64_t)blockIdx.x * L2_CHUNK, r1 = min(n, r0 + L2_CHUNK);
-    for (uint32_t d = threadIdx.x; d < F; d += THREADS) em.init(d, O[(uint64_t)d * nch + blockIdx.x]);
-    if (threadIdx.x == 0) *nflush = 0;
-    uint64_t v[RPT];
-#pragma unroll
-    for (int q = 0; q < RPT; q++) {
-        const uint64_t idx = r0 + (uint64_t)q * THREADS + threadIdx.x;
-        v[q] = idx < min(r1, r0 + TILE) ? rec_in[idx] : ~0ull;
-    }
-    const uint32_t ntiles = uniform_u32((uint32_t)((r1 - r0 + TILE - 1) / TILE));
-    for (uint32_t ti = 0; ti < ntiles; ti++) {
-        const uint64_t t0 = r0 + (uint64_t)ti * TILE;
-        const bool last = ti + 1 == ntiles;
-        block_sync();
-        uint32_t rank[RPT];
-        uint64_t x[RPT];
-#pragma unroll
-        for (int q = 0; q < RPT; q++) {
-            x[q] = v[q];
-            if (x[q] != ~0ull) {
-                rank[q] = atomicAdd(&hist[(uint32_t)x[q] >> shift], 1u);
-                em.note((uint32_t)x[q] >> shift, rank[q], last);
-            }
-        }
-        {
-            const uint64_t n0 = t0 + TILE, n1 = min(r1, n0 + TILE);
-#pragma unroll
-            for (int q = 0; q < RPT; q++) {
-                const uint64_t idx = n0 + (uint64_t)q * THREADS + threadIdx.x;
-                v[q] = idx < n1 ? rec_in[idx] : ~0ull;
-            }
-        }
-        block_sync();
-        em.flush_listed(F, last, rec_out);
-        block_sync();
-#pragma unroll
-        for (int q = 0; q < RPT; q++)
-            if (x[q] != ~0ull)
-                em.put_rank((uint32_t)x[q] >> shift, rank[q], (x[q] & ~0xFFFFFFFFull) | (x[q] & omask), last,
-                            rec_out);
-        block_sync();
-        em.advance(F, last);
-    }
 }
 
 // ---------------------------------------------------------------------------

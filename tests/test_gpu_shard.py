@@ -89,3 +89,18 @@ def test_group_slices_cover_tables():
             assert los[l][0] + los[l][1] == los[l + 1][0] and los[l + 1][0] % 8 == 0
         assert [g.slice(l, i) for l in range(5)] == [parallel.shard_slices(sizes, 5)[l][i] for l in range(5)]
     g.close()
+
+
+@pytest.mark.parametrize("mode", ["no-filter", "filter-rerun"])
+def test_loopback_owned_filter_modes(mode, monkeypatch):
+    """The 4-way group without the owned-record filter (every shard hashes
+    twice), and with a first filter buffer too small for the owned records
+    (the filter re-runs into a larger one); both must equal the oracle."""
+    if mode == "no-filter":
+        monkeypatch.setenv("KH_OWN_FILTER_MIN", "0")
+    else:
+        monkeypatch.setenv("KH_OWN_FILTER_FRAC", "0.3")
+    sizes = O.get_n_primes_near_x(4, 200003)
+    g, o = run_pair("Countgraph", 21, sizes, 4, nreads=4000, L=150, batch=1 << 17, bigcount=True)
+    assert_group_equals_oracle(g, o, sizes, True)
+    g.close()
