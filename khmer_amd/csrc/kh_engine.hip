@@ -129,6 +129,13 @@ static void ensure_recs(Graph *g, uint64_t recs) {
     for (uint64_t **pp : {&w.rec1, &w.rec2}) {
         if (*pp) KH_HIP(hipFree(*pp));
         *pp = nullptr;
+        // KH_REC_MALLOC_FLAGS: development knob, hipExtMallocWithFlags flags for
+        // the record buffers (placement experiments); plain hipMalloc otherwise
+        static const char *fl = getenv("KH_REC_MALLOC_FLAGS");
+        if (fl && atoi(fl) &&
+            hipExtMallocWithFlags((void **)pp, cap * 8 + 64, (unsigned)atoi(fl)) == hipSuccess)
+            continue;
+        (void)hipGetLastError();
         KH_HIP(hipMalloc((void **)pp, cap * 8 + 64));
     }
     w.cap_recs = cap;
