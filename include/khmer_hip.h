@@ -176,6 +176,11 @@ int kh_graph_load_tagset(kh_graph *g, const char *path, int clear);
  * contiguously (nreads*read_len/32 + 2 words), k-mer offsets r*(read_len-k+1). */
 int kh_synth_packed_device(int device, uint64_t seed, uint64_t r0, uint64_t nreads, int read_len, int k,
                            uint64_t *d_words, uint64_t *d_kmer_off);
+/* the skewed "genomic" stream of SURVEY.md §8(d) (khmer_amd/synth.py
+ * genomic_codes): reads sampled from a random genome of `genome` bases, either
+ * strand, 1% substitutions; same packing as kh_synth_packed_device. */
+int kh_synth_genomic_device(int device, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int read_len,
+                            int k, uint64_t *d_words, uint64_t *d_kmer_off);
 int kh_device_malloc(int device, uint64_t bytes, void **out);
 int kh_device_free(int device, void *p);
 int kh_device_synchronize(int device);

@@ -85,6 +85,7 @@ SIGNATURES = {
     "kh_graph_save_tagset": (i32, [P, ctypes.c_char_p]),
     "kh_graph_load_tagset": (i32, [P, ctypes.c_char_p, i32]),
     "kh_synth_packed_device": (i32, [i32, u64, u64, u64, i32, i32, P, P]),
+    "kh_synth_genomic_device": (i32, [i32, u64, u64, u64, u64, i32, i32, P, P]),
     "kh_device_malloc": (i32, [i32, u64, ctypes.POINTER(P)]),
     "kh_device_free": (i32, [i32, P]),
     "kh_device_synchronize": (i32, [i32]),

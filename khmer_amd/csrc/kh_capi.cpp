@@ -27,8 +27,8 @@ bool parser_is_complete(Parser *p);
 void parser_fill_batch(Parser *p, HostBatch &b, int k, uint64_t max_kmers, uint64_t max_bases, bool *done,
                        uint64_t *taken);
 void engine_hash_batch(Graph *g, const HostBatch &b, uint64_t *h_out);
-void engine_synth_packed(int device, uint64_t seed, uint64_t r0, uint64_t nreads, int L, int k, uint64_t *d_words,
-                         uint64_t *d_koff);
+void engine_synth_packed(int device, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L, int k,
+                         uint64_t *d_words, uint64_t *d_koff);
 }  // namespace kh
 
 using namespace kh;
@@ -420,17 +420,10 @@ int kh_add_hashes(kh_graph *h, const uint64_t *hashes, uint64_t n, uint8_t *is_n
         std::lock_guard<std::recursive_mutex> lk(g->mu);
         KH_HIP(hipSetDevice(g->device));
         if (!n) return;
-        uint64_t *d = nullptr;
-        KH_HIP(hipMalloc((void **)&d, n * 8));
-        KH_HIP(hipMemcpy(d, hashes, n * 8, hipMemcpyHostToDevice));
+        DevBuf d(n * 8);
+        KH_HIP(hipMemcpy(d.p, hashes, n * 8, hipMemcpyHostToDevice));
         PassOut out{is_new, nullptr};
-        try {
-            engine_consume_hashes(g, d, n, is_new ? &out : nullptr);
-        } catch (...) {
-            (void)hipFree(d);
-            throw;
-        }
-        KH_HIP(hipFree(d));
+        engine_consume_hashes(g, d.as<uint64_t>(), n, is_new ? &out : nullptr);
     });
 }
 
@@ -503,12 +496,10 @@ int kh_abundance_distribution(kh_graph *h, kh_parser *ph, kh_graph *th, uint64_t
             std::vector<uint64_t> hs(nk);
             engine_hash_batch(g, b, hs.data());
             std::vector<uint8_t> isnew(nk);
-            uint64_t *d = nullptr;
-            KH_HIP(hipMalloc((void **)&d, nk * 8));
-            KH_HIP(hipMemcpy(d, hs.data(), nk * 8, hipMemcpyHostToDevice));
+            DevBuf d(nk * 8);
+            KH_HIP(hipMemcpy(d.p, hs.data(), nk * 8, hipMemcpyHostToDevice));
             PassOut out{isnew.data(), nullptr};
-            engine_consume_hashes(t, d, nk, &out);
-            KH_HIP(hipFree(d));
+            engine_consume_hashes(t, d.as<uint64_t>(), nk, &out);   // passes of t's batch size, in order
             std::vector<uint64_t> sel;
             for (uint64_t j = 0; j < nk; j++)
                 if (isnew[j]) sel.push_back(hs[j]);
@@ -679,15 +670,23 @@ extern "C" int kh_graph_load(const char *path, int expected_storage, int hash_ki
         in.read(&n, 1);
         in.read(&occ, 8);
         if (n < 1) fail(KH_EFILE, std::string("Unexpected end of k-mer graph file: ") + path);
+        if (n > MAXT) fail(KH_EFILE, std::string("too many tables in k-mer graph file: ") + path);
         std::vector<uint64_t> sizes;
         std::vector<std::vector<uint8_t>> tabs;
         for (int i = 0; i < n; i++) {
             uint64_t sz = 0;
             in.read(&sz, 8);
+            if (sz == 0) fail(KH_EFILE, std::string("zero-sized table in k-mer graph file: ") + path);
             uint64_t nb = type == BIT ? sz / 8 + 1 : type == NIBBLE ? sz / 2 + 1 : sz;
             sizes.push_back(sz);
-            tabs.emplace_back(nb);
-            in.read(tabs.back().data(), nb);
+            tabs.emplace_back();
+            // bounded chunks: a header that claims more than the file holds
+            // fails at end of file rather than allocating the claimed size
+            for (uint64_t a = 0; a < nb; a += (64u << 20)) {
+                const uint64_t m = std::min<uint64_t>(64u << 20, nb - a);
+                tabs.back().resize(a + m);
+                in.read(tabs.back().data() + a, m);
+            }
         }
         std::vector<std::pair<uint64_t, uint16_t>> bcs;
         if (type == BYTE) {
@@ -724,12 +723,17 @@ extern "C" int kh_graph_load(const char *path, int expected_storage, int hash_ki
 extern "C" {
 
 int kh_graph_n_tags(kh_graph *h, uint64_t *out) {
-    return guard([&] { CHECK_PTR(h); *out = h->g->tags.size(); });
+    return guard([&] {
+        CHECK_PTR(h);
+        std::lock_guard<std::recursive_mutex> lk(h->g->mu);
+        *out = h->g->tags.size();
+    });
 }
 
 int kh_graph_get_tags(kh_graph *h, uint64_t *out) {
     return guard([&] {
         CHECK_PTR(h);
+        std::lock_guard<std::recursive_mutex> lk(h->g->mu);
         std::vector<uint64_t> v(h->g->tags.begin(), h->g->tags.end());
         std::sort(v.begin(), v.end());
         memcpy(out, v.data(), v.size() * 8);
@@ -737,7 +741,11 @@ int kh_graph_get_tags(kh_graph *h, uint64_t *out) {
 }
 
 int kh_graph_add_tag(kh_graph *h, uint64_t t) {
-    return guard([&] { CHECK_PTR(h); h->g->tags.insert(t); });
+    return guard([&] {
+        CHECK_PTR(h);
+        std::lock_guard<std::recursive_mutex> lk(h->g->mu);
+        h->g->tags.insert(t);
+    });
 }
 
 // Hashgraph::save_tagset (src/oxli/hashgraph.cc:55-88); std::set order = ascending
@@ -745,6 +753,7 @@ int kh_graph_save_tagset(kh_graph *h, const char *path) {
     return guard([&] {
         CHECK_PTR(h);
         Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
         std::vector<uint64_t> v(g->tags.begin(), g->tags.end());
         std::sort(v.begin(), v.end());
         Out o;
@@ -770,6 +779,7 @@ int kh_graph_load_tagset(kh_graph *h, const char *path, int clear) {
     return guard([&] {
         CHECK_PTR(h);
         Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
         In in;
         in.path = path;
         in.gz = gzopen(path, "rb");
@@ -789,8 +799,15 @@ int kh_graph_load_tagset(kh_graph *h, const char *path, int clear) {
         in.read(&n, 8);
         in.read(&density, 4);
         if ((int)k != g->k) fail(KH_EFILE, "Incorrect k-mer size in tagset file");
-        std::vector<uint64_t> v(n);
-        in.read(v.data(), n * 8);
+        // read in bounded chunks: a corrupt count fails at end of file instead
+        // of allocating whatever the header claims
+        std::vector<uint64_t> v;
+        for (uint64_t a = 0; a < n; a += (1u << 20)) {
+            const uint64_t m = std::min<uint64_t>(1u << 20, n - a);
+            const size_t old = v.size();
+            v.resize(old + m);
+            in.read(v.data() + old, m * 8);
+        }
         if (clear) g->tags.clear();
         g->tags.insert(v.begin(), v.end());
     });
@@ -803,7 +820,16 @@ extern "C" int kh_synth_packed_device(int device, uint64_t seed, uint64_t r0, ui
                                       uint64_t *d_words, uint64_t *d_kmer_off) {
     return guard([&] {
         if (read_len < k || k < 1 || k > 32) fail(KH_EVALUE, "need 1 <= k <= read length and k <= 32");
-        engine_synth_packed(device, seed, r0, nreads, read_len, k, d_words, d_kmer_off);
+        engine_synth_packed(device, seed, 0, r0, nreads, read_len, k, d_words, d_kmer_off);
+    });
+}
+
+extern "C" int kh_synth_genomic_device(int device, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads,
+                                       int read_len, int k, uint64_t *d_words, uint64_t *d_kmer_off) {
+    return guard([&] {
+        if (read_len < k || k < 1 || k > 32) fail(KH_EVALUE, "need 1 <= k <= read length and k <= 32");
+        if (genome < (uint64_t)read_len) fail(KH_EVALUE, "genome shorter than a read");
+        engine_synth_packed(device, seed, genome, r0, nreads, read_len, k, d_words, d_kmer_off);
     });
 }
 

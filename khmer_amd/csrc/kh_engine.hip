@@ -685,14 +685,20 @@ void engine_consume_bytes(Graph *g, const uint8_t *d_bytes, const uint64_t *d_ko
     consume_reads(g, src_bytes(g, d_bytes), d_koff, nreads, nkmers, 0, out);
 }
 
+// Passes run in stream order, so per-k-mer outputs of consecutive passes are
+// exact when each pass writes its own slice of them.
 void engine_consume_hashes(Graph *g, const uint64_t *d_hashes, uint64_t n, const PassOut *out) {
-    const uint64_t B = g->batch_kmers;
-    if (n > B && out) fail(KH_EVALUE, "per-k-mer outputs need a single device batch");
+    const uint64_t B = std::min<uint64_t>(g->batch_kmers, MAX_PASS_KMERS);
     for (uint64_t a = 0; a < n; a += B) {
         SrcHashes s{};
         s.h = d_hashes + a;
         s.k = g->k;
-        run_pass(g, s, std::min(B, n - a), out);
+        PassOut o;
+        if (out) {
+            o.h_new = out->h_new ? out->h_new + a : nullptr;
+            o.h_hash = out->h_hash ? out->h_hash + a : nullptr;
+        }
+        run_pass(g, s, std::min(B, n - a), out ? &o : nullptr);
     }
 }
 
@@ -734,8 +740,8 @@ void engine_hash_batch(Graph *g, const HostBatch &b, uint64_t *h_out) {
     const uint64_t nk = b.nkmers(), nr = b.nreads();
     if (!nk) return;
     upload_batch(g, b);
-    uint64_t *d = nullptr;
-    KH_HIP(hipMalloc((void **)&d, nk * 8));
+    DevBuf dbuf(nk * 8);
+    uint64_t *d = dbuf.as<uint64_t>();
     const uint64_t tiles = (nk + Q_TILE - 1) / Q_TILE;
     const size_t lds = 16 + (Q_TILE + 2) * 8;
     if (b.hash == MURMUR) {
@@ -753,7 +759,6 @@ void engine_hash_batch(Graph *g, const HostBatch &b, uint64_t *h_out) {
     KH_HIP(hipGetLastError());
     KH_HIP(hipMemcpyAsync(h_out, d, nk * 8, hipMemcpyDeviceToHost, g->stream));
     KH_HIP(hipStreamSynchronize(g->stream));
-    KH_HIP(hipFree(d));
 }
 
 uint64_t engine_consume_filtered(Graph *g, const HostBatch &b, const BandMask &f) {
@@ -775,13 +780,9 @@ uint64_t engine_consume_filtered(Graph *g, const HostBatch &b, const BandMask &f
         F.consume_masked = f.consume_masked;
     }
     upload_batch(g, b);
-    uint64_t *d_h = nullptr, *d_sel = nullptr, *d_n = nullptr;
-    uint8_t *d_keep = nullptr;
-    void *tmp = nullptr;
-    KH_HIP(hipMalloc((void **)&d_h, nk * 8));
-    KH_HIP(hipMalloc((void **)&d_sel, nk * 8));
-    KH_HIP(hipMalloc((void **)&d_keep, nk));
-    KH_HIP(hipMalloc((void **)&d_n, 8));
+    DevBuf b_h(nk * 8), b_sel(nk * 8), b_keep(nk), b_n(8), b_tmp;
+    uint64_t *d_h = b_h.as<uint64_t>(), *d_sel = b_sel.as<uint64_t>(), *d_n = b_n.as<uint64_t>();
+    uint8_t *d_keep = b_keep.as<uint8_t>();
     const uint64_t tiles = (nk + Q_TILE - 1) / Q_TILE;
     const size_t lds = 16 + (Q_TILE + 2) * 8;
     if (b.hash == MURMUR) {
@@ -800,14 +801,13 @@ uint64_t engine_consume_filtered(Graph *g, const HostBatch &b, const BandMask &f
     KH_HIP(hipGetLastError());
     size_t bytes = 0;
     KH_HIP(rocprim::select(nullptr, bytes, d_h, d_keep, d_sel, d_n, (size_t)nk, g->stream));
-    KH_HIP(hipMalloc(&tmp, bytes));
-    KH_HIP(rocprim::select(tmp, bytes, d_h, d_keep, d_sel, d_n, (size_t)nk, g->stream));
+    b_tmp.alloc(bytes);
+    KH_HIP(rocprim::select(b_tmp.p, bytes, d_h, d_keep, d_sel, d_n, (size_t)nk, g->stream));
     uint64_t kept = 0;
     KH_HIP(hipMemcpyAsync(&kept, d_n, 8, hipMemcpyDeviceToHost, g->stream));
     KH_HIP(hipStreamSynchronize(g->stream));
     if (kept) engine_consume_hashes(g, d_sel, kept, nullptr);
     KH_HIP(hipStreamSynchronize(g->stream));
-    for (void *p : {(void *)d_h, (void *)d_sel, (void *)d_keep, (void *)d_n, tmp}) KH_HIP(hipFree(p));
     return kept;
 }
 
@@ -833,12 +833,9 @@ void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, floa
     if (!nr) return;
     engine_sync_bigcounts(g);
     upload_batch(g, b);
-    uint16_t *d_counts = nullptr, *d_med = nullptr;
-    float *d_avg = nullptr, *d_sd = nullptr;
-    KH_HIP(hipMalloc((void **)&d_counts, nk * 2 + 64));
-    KH_HIP(hipMalloc((void **)&d_med, nr * 2 + 64));
-    KH_HIP(hipMalloc((void **)&d_avg, nr * 4 + 64));
-    KH_HIP(hipMalloc((void **)&d_sd, nr * 4 + 64));
+    DevBuf b_counts(nk * 2 + 64), b_med(nr * 2 + 64), b_avg(nr * 4 + 64), b_sd(nr * 4 + 64);
+    uint16_t *d_counts = b_counts.as<uint16_t>(), *d_med = b_med.as<uint16_t>();
+    float *d_avg = b_avg.as<float>(), *d_sd = b_sd.as<float>();
     const uint64_t tiles = (nk + Q_TILE - 1) / Q_TILE;
     const size_t lds = 16 + (Q_TILE + 2) * 8;
     if (tiles) {
@@ -863,7 +860,6 @@ void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, floa
     KH_HIP(hipMemcpyAsync(avg, d_avg, nr * 4, hipMemcpyDeviceToHost, g->stream));
     KH_HIP(hipMemcpyAsync(sd, d_sd, nr * 4, hipMemcpyDeviceToHost, g->stream));
     KH_HIP(hipStreamSynchronize(g->stream));
-    for (void *p : {(void *)d_counts, (void *)d_med, (void *)d_avg, (void *)d_sd}) KH_HIP(hipFree(p));
 }
 
 void engine_download_table(Graph *g, int i, uint8_t *dst) {
@@ -876,12 +872,17 @@ void engine_upload_table(Graph *g, int i, const uint8_t *src) {
     KH_HIP(hipStreamSynchronize(g->stream));
 }
 
-void engine_synth_packed(int device, uint64_t seed, uint64_t r0, uint64_t nreads, int L, int k, uint64_t *d_words,
-                         uint64_t *d_koff) {
+void engine_synth_packed(int device, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L, int k,
+                         uint64_t *d_words, uint64_t *d_koff) {
     KH_HIP(hipSetDevice(device));
     const uint64_t nwords = (nreads * (uint64_t)L + 31) / 32 + 1;
     const unsigned grid = (unsigned)std::min<uint64_t>((nwords + 255) / 256, 1u << 16);
-    hipLaunchKernelGGL(k_synth_packed, dim3(grid), dim3(256), 0, 0, seed, r0, nreads, L, k, d_words, nwords, d_koff);
+    if (genome)
+        hipLaunchKernelGGL(k_synth_genomic, dim3(grid), dim3(256), 0, 0, seed, genome, r0, nreads, L, k, d_words,
+                           nwords, d_koff);
+    else
+        hipLaunchKernelGGL(k_synth_packed, dim3(grid), dim3(256), 0, 0, seed, r0, nreads, L, k, d_words, nwords,
+                           d_koff);
     KH_HIP(hipGetLastError());
     KH_HIP(hipDeviceSynchronize());
 }
@@ -1402,6 +1403,18 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
                 sb.rbase = 0;
                 srcs[l] = sb;
                 ps[l] = pass_stage_a(g, sb, nr * kpr);
+            }
+            if (r0 == 0 && s + 1 < W) {
+                // No comm_b broadcast is ever in flight together with an
+                // operation on G->comm: broadcast s+1 starts after source
+                // s-1's last pass (ev_free) and must finish before source s's
+                // first collective.  Same order on every rank, so the two
+                // communicators' kernels never wait on each other.  It still
+                // overlaps the first pass's hashing and level-1 work.
+                for (int l = 0; l < NL; l++) {
+                    KH_HIP(hipSetDevice(G->shards[l]->device));
+                    KH_HIP(hipStreamWaitEvent(G->shards[l]->stream, G->loc[l].ev_ready[(s + 1) & 1], 0));
+                }
             }
             group_route_winners(G, ps);
             if (ps[0].bigc) group_merge_full(G, ps);

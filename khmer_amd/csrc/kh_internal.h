@@ -34,6 +34,21 @@ struct Error : std::runtime_error {
         }                                                                                   \
     } while (0)
 
+// device scratch owned by a scope: freed on every path, including throws
+struct DevBuf {
+    void *p = nullptr;
+    DevBuf() = default;
+    explicit DevBuf(size_t bytes) { alloc(bytes); }
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    void alloc(size_t bytes) {
+        if (p) { (void)hipFree(p); p = nullptr; }
+        KH_HIP(hipMalloc(&p, bytes ? bytes : 1));
+    }
+    template <class T> T *as() const { return (T *)p; }
+};
+
 constexpr int MAXT = 32;  // tables per graph on device (NibbleStorage's own cap, storage.hh:290)
 // k-mers of one device pass: at most 2560 winner windows of 2^20 k-mers (the
 // LDS of k_scatter_w's per-window tails and k_mark's 2^20-bit bitmap); batch

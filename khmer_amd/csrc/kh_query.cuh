@@ -249,4 +249,43 @@ __global__ void k_synth_packed(uint64_t seed, uint64_t r0, uint64_t nreads, int 
         koff[r] = r * (uint64_t)(L - k + 1);
 }
 
+// genomic stream (khmer_amd/synth.py genomic_codes): read r samples L bases at
+// a uniform start (either strand) of a random genome of G bases (seed+1) and
+// substitutes 1% of them (seed+3).  One output word per thread; the genome word
+// and the read's (start, strand) are cached across the word's 32 bases.
+__global__ void k_synth_genomic(uint64_t seed, uint64_t G, uint64_t r0, uint64_t nreads, int L, int k,
+                                uint64_t *words, uint64_t nwords, uint64_t *koff) {
+    const uint64_t nbases = nreads * (uint64_t)L;
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nwords;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t out = 0;
+        uint64_t cur_r = ~0ull, start = 0, gw_key = ~0ull, gsrc = 0;
+        bool rc = false;
+        for (int b = 0; b < 32; b++) {
+            const uint64_t p = w * 32 + b;
+            uint64_t code = 0;
+            if (p < nbases) {
+                const uint64_t r = p / (uint64_t)L, i = p % (uint64_t)L;
+                if (r != cur_r) {
+                    cur_r = r;
+                    start = synth_word(seed + 2, r0 + r, 0) % (G - (uint64_t)L + 1);
+                    rc = synth_word(seed + 2, r0 + r, 1) & 1;
+                }
+                const uint64_t gi = rc ? start + (uint64_t)L - 1 - i : start + i;
+                const uint64_t gw = gi >> 5;
+                if (gw != gw_key) { gsrc = synth_word(seed + 1, gw >> 20, gw & 0xFFFFF); gw_key = gw; }
+                code = (gsrc >> (62 - 2 * (gi & 31))) & 3;
+                if (rc) code ^= 1;
+                const uint64_t u = synth_word(seed + 3, r0 + r, i);
+                if (u % 100 == 0) code = (code + 1 + (u >> 32) % 3) & 3;
+            }
+            out = (out << 2) | code;
+        }
+        words[w] = out;
+    }
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r <= nreads;
+         r += (uint64_t)gridDim.x * blockDim.x)
+        koff[r] = r * (uint64_t)(L - k + 1);
+}
+
 }  // namespace kh

@@ -61,3 +61,38 @@ def batch(r0, nreads, length, seed=SEED):
     rows = read_ascii(r0, nreads, length, seed)
     offs = np.arange(nreads + 1, dtype=np.uint64) * np.uint64(length)
     return rows.tobytes(), offs
+
+
+def _word(seed, r, t):
+    """synth word(s) for arrays r, t (broadcast), uint64."""
+    with np.errstate(over="ignore"):
+        key = np.uint64(seed) + (np.asarray(r, dtype=np.uint64) * np.uint64(1 << 20)
+                                 + np.asarray(t, dtype=np.uint64)) * GOLDEN
+    return _mix(np.atleast_1d(key))
+
+
+def genomic_codes(r0, nreads, length, genome, seed=SEED):
+    """Skewed stream (SURVEY.md §8(d) "genomic"): read r takes `length` bases at
+    start = word(seed+2, r, 0) % (genome - length + 1) of a random genome
+    (base g = 2-bit code of word(seed+1, (g>>5)>>20, (g>>5)&0xFFFFF)), reverse
+    complemented when word(seed+2, r, 1) is odd; base i is substituted when
+    u = word(seed+3, r, i) is 0 mod 100, by (code + 1 + (u>>32) % 3) & 3."""
+    r = np.arange(r0, r0 + nreads, dtype=np.uint64)
+    start = _word(seed + 2, r, 0) % np.uint64(genome - length + 1)
+    rc = (_word(seed + 2, r, 1) & np.uint64(1)).astype(bool)
+    i = np.arange(length, dtype=np.uint64)[None, :]
+    gi = np.where(rc[:, None], start[:, None] + np.uint64(length - 1) - i, start[:, None] + i)
+    gw = gi >> np.uint64(5)
+    src = _word(seed + 1, gw >> np.uint64(20), gw & np.uint64(0xFFFFF)).reshape(gi.shape)
+    code = (src >> (np.uint64(62) - np.uint64(2) * (gi & np.uint64(31)))) & np.uint64(3)
+    code = np.where(rc[:, None], code ^ np.uint64(1), code)
+    u = _word(seed + 3, r[:, None], i).reshape(gi.shape)
+    sub = (u % np.uint64(100)) == 0
+    code = np.where(sub, (code + np.uint64(1) + (u >> np.uint64(32)) % np.uint64(3)) & np.uint64(3), code)
+    return code.astype(np.uint8)
+
+
+def genomic_batch(r0, nreads, length, genome, seed=SEED):
+    rows = _ASCII[genomic_codes(r0, nreads, length, genome, seed)]
+    offs = np.arange(nreads + 1, dtype=np.uint64) * np.uint64(length)
+    return rows.tobytes(), offs

@@ -941,3 +941,59 @@ uint64_t or_consume_batch_mt(or_table *t, const char *seqs, const uint64_t *offs
     for (int i = 0; i < nthreads; i++) { pthread_join(th[i], NULL); total += jobs[i].kmers; }
     return total;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Synthetic input streams.  These are NOT reference
+ * functions: they regenerate, on the host, the exact read streams the
+ * benchmark generates in HBM (khmer_amd/synth.py defines them; the device
+ * twins are kh_query.cuh k_synth_packed / k_synth_genomic), so that the oracle
+ * can consume the benchmark's own workload for full-size golden fixtures.
+ * Codes: A=0 T=1 C=2 G=3 (twobit_repr, include/oxli/kmer_hash.hh:62-73). */
+static inline uint64_t synth_word(uint64_t seed, uint64_t r, uint64_t t) {
+    uint64_t z = seed + ((r << 20) + t) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+static const char synth_ascii[4] = { 'A', 'T', 'C', 'G' };
+
+void or_synth_read(uint64_t seed, uint64_t r, int L, char *out) {
+    for (int i = 0; i < L; i++)
+        out[i] = synth_ascii[(synth_word(seed, r, (uint64_t)i >> 5) >> (62 - 2 * (i & 31))) & 3];
+    out[L] = 0;
+}
+
+/* genomic stream: reads of L bases sampled uniformly (either strand) from a
+ * random genome of G bases (seed+1), with a 1% substitution rate (seed+3). */
+static inline unsigned genome_base(uint64_t seed, uint64_t g) {
+    const uint64_t w = g >> 5;
+    return (unsigned)((synth_word(seed + 1, w >> 20, w & 0xFFFFF) >> (62 - 2 * (g & 31))) & 3);
+}
+
+void or_synth_genomic_read(uint64_t seed, uint64_t G, uint64_t r, int L, char *out) {
+    const uint64_t start = synth_word(seed + 2, r, 0) % (G - (uint64_t)L + 1);
+    const int rc = (int)(synth_word(seed + 2, r, 1) & 1);
+    for (int i = 0; i < L; i++) {
+        unsigned c = rc ? (genome_base(seed, start + (uint64_t)(L - 1 - i)) ^ 1u)
+                        : genome_base(seed, start + (uint64_t)i);
+        const uint64_t u = synth_word(seed + 3, r, (uint64_t)i);
+        if (u % 100 == 0) c = (unsigned)((c + 1 + (u >> 32) % 3) & 3);
+        out[i] = synth_ascii[c];
+    }
+    out[L] = 0;
+}
+
+/* consume reads r0..r0+nreads-1 of a synthetic stream in stream order
+ * (genome == 0: iid uniform stream; otherwise the genomic stream) */
+uint64_t or_consume_synth(or_table *t, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L) {
+    char *buf = malloc((size_t)L + 1);
+    uint64_t total = 0;
+    for (uint64_t r = r0; r < r0 + nreads; r++) {
+        if (genome) or_synth_genomic_read(seed, genome, r, L, buf);
+        else or_synth_read(seed, r, L, buf);
+        total += or_consume_string(t, buf, (size_t)L);
+    }
+    free(buf);
+    return total;
+}

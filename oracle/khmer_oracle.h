@@ -106,6 +106,12 @@ const char *or_last_error(void);
 uint64_t  or_consume_batch_mt(or_table *t, const char *seqs, const uint64_t *offs,
                               uint64_t nreads, int nthreads);
 
+/* ---- synthetic streams of khmer_amd/synth.py (NOT reference functions; they
+ * let the oracle consume the benchmark's exact workload for golden fixtures) ---- */
+void      or_synth_read(uint64_t seed, uint64_t r, int L, char *out /* L+1 */);
+void      or_synth_genomic_read(uint64_t seed, uint64_t genome, uint64_t r, int L, char *out /* L+1 */);
+uint64_t  or_consume_synth(or_table *t, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L);
+
 #ifdef __cplusplus
 }
 #endif

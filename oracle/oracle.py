@@ -73,6 +73,9 @@ def lib():
             "or_parser_num_reads": (u64, [P]),
             "or_parser_close": (None, [P]),
             "or_last_error": (ctypes.c_char_p, []),
+            "or_synth_read": (None, [u64, u64, i32, ctypes.c_char_p]),
+            "or_synth_genomic_read": (None, [u64, u64, u64, i32, ctypes.c_char_p]),
+            "or_consume_synth": (u64, [P, u64, u64, u64, u64, i32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -204,6 +207,17 @@ class Table:
             return lib().or_consume_batch_mt(self._h, seqs, arr, len(offs) - 1, threads)
         return lib().or_consume_batch(self._h, seqs, arr, len(offs) - 1)
 
+    def consume_synth(self, seed, r0, nreads, length, genome=0):
+        """Consume reads r0.. of the benchmark's synthetic stream (khmer_amd/synth.py),
+        in stream order; genome > 0 selects the genomic stream."""
+        return lib().or_consume_synth(self._h, seed, genome, r0, nreads, length)
+
+    def table_view(self, i):
+        """Zero-copy read-only view of table i (for digests of GB tables)."""
+        n = lib().or_table_nbytes(self._h, i)
+        p = lib().or_table_data(self._h, i)
+        return memoryview((ctypes.c_uint8 * n).from_address(ctypes.addressof(p.contents))).cast("B")
+
     def median(self, seq):
         m, a, s = ctypes.c_uint16(), ctypes.c_float(), ctypes.c_float()
         if lib().or_median(self._h, _b(seq), len(seq), ctypes.byref(m), ctypes.byref(a),
@@ -251,6 +265,15 @@ class Table:
     def save_tagset(self, path):
         if lib().or_save_tagset(self._h, _b(path)) != 0:
             raise OSError(err())
+
+
+def synth_read(seed, r, length, genome=0):
+    buf = ctypes.create_string_buffer(length + 1)
+    if genome:
+        lib().or_synth_genomic_read(seed, genome, r, length, buf)
+    else:
+        lib().or_synth_read(seed, r, length, buf)
+    return buf.raw[:length]
 
 
 def read_fastx(path):

@@ -203,6 +203,42 @@ def test_abundance_distribution():
     assert dist == o.abundance_distribution(data("random-20-a.fa"), O.Table(O.BIT, 12, sizes))
 
 
+@pytest.mark.parametrize("batch", [(1024, 1024), (1024, 4096), (4096, 1024)])
+def test_abundance_distribution_many_passes(batch):
+    """Parser batches larger than the tracking table's device pass:
+    is-new flags come from several in-order passes and must stay exact."""
+    from khmer_amd._lib import lib, check
+    sizes = [1000003, 1009837, 1000005]
+    g = khmer.Countgraph(12, 1, 1, primes=sizes)
+    g.consume_seqfile(data("random-20-a.fa"))
+    tracking = khmer.Nodegraph(12, 1, 1, primes=sizes)
+    check(lib.kh_graph_set_batch_kmers(g._g, batch[0]))
+    check(lib.kh_graph_set_batch_kmers(tracking._g, batch[1]))
+    dist = g.abundance_distribution(data("random-20-a.fa"), tracking)
+    o = O.Table(O.BYTE, 12, sizes)
+    o.consume_fastx(data("random-20-a.fa"))
+    assert sum(dist) == 3966
+    assert dist == o.abundance_distribution(data("random-20-a.fa"), O.Table(O.BIT, 12, sizes))
+
+
+def test_add_hashes_is_new_many_passes():
+    """kh_add_hashes with per-hash is_new over more hashes than one pass."""
+    import ctypes
+    import random
+    from khmer_amd._lib import lib, check
+    sizes = [10007, 10009]
+    g = khmer.Countgraph(12, 1, 1, primes=sizes)
+    check(lib.kh_graph_set_batch_kmers(g._g, 1024))
+    rng = random.Random(7)
+    hs = [rng.randrange(1 << 24) for _ in range(5000)]
+    arr = (ctypes.c_uint64 * len(hs))(*hs)
+    isnew = (ctypes.c_uint8 * len(hs))()
+    check(lib.kh_add_hashes(g._g, arr, len(hs), isnew))
+    o = O.Table(O.BYTE, 12, sizes)
+    assert list(isnew) == [o.add(h) for h in hs]
+    assert g.n_unique_kmers() == o.n_unique_kmers()
+
+
 @pytest.mark.parametrize("cls", ["Countgraph", "SmallCountgraph", "Nodegraph"])
 @pytest.mark.parametrize("suffix", ["", ".gz"])
 def test_save_matches_oracle_and_loads(tmp_path, cls, suffix):
