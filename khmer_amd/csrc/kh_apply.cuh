@@ -27,8 +27,11 @@ struct ApplyArgs {
     uint32_t *win;        // winners of region rr at win[e0(rr) ...]
     uint32_t *wcnt;       // [regions] winners per region
     uint8_t *fullf;
-    uint64_t *cross;
-    uint64_t cap_cross;
+    // crossing bins (bigcount): region rr's entries (offset << 8 | c0) at
+    // xent[e0(rr) ...] (a crossing bin holds >= 2 of the region's records, so
+    // they fit), one segment descriptor per region with crossings in xseg
+    uint32_t *xent;
+    uint4 *xseg;
     uint64_t *ctr;
     uint64_t rprefix[MAXT + 1];   // real-region prefix per table
 };
@@ -217,7 +220,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
         if (t < R / 512) chg[t] = 0;
         if (bigc) {
             for (uint32_t x = t; x < R / 32; x += blockDim.x) full255[x] = 0;
-            if (t == 0) s_flag[0] = 0;
+            if (t == 0) s_flag[0] = s_flag[1] = 0;
         }
         PH(5);
         block_sync();
@@ -285,9 +288,8 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
                 else inval |= 1u << k;
                 if (bigc && c == 255) full |= 1u << k;
                 if (bigc && c < 255 && v > 255 && !(P.ablate & 8)) {   // insert r sees c + r: full iff c + r >= 255, r < n
-                    const uint64_t idx = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
-                    if (idx < A.cap_cross) A.cross[idx] = ((P.tbase[ri.i] + ri.bin_lo + o + k) << 8) | c;
-                    else atomicOr((unsigned long long *)&A.ctr[CTR_ERR], 1ull);
+                    const uint32_t idx = atomicAdd(&s_flag[1], 1u);
+                    A.xent[ri.e0 + idx] = ((o + k) << 8) | c;
                 }
             }
             const bool changed = fw != cw;
@@ -325,6 +327,10 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
         const uint32_t wex = wave_winner_scan(nw, s_wt);
         block_sync();
         PH(2);
+        if (bigc && t == 0 && s_flag[1]) {
+            const uint64_t seg = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
+            A.xseg[seg] = make_uint4((uint32_t)ri.e0, (uint32_t)(ri.e0 >> 32), (uint32_t)(ri.e1 - ri.e0), s_flag[1]);
+        }
         prefetch_region<KIND>(P, A, rr + gridDim.x, total, bnext, nxt);
         bnext = bafter;
         // pass 2: write back changed 16-bin chunks; winners to the region's segment
@@ -627,68 +633,106 @@ __global__ void __launch_bounds__(PT_THREADS) k_mark(const uint32_t *wout, const
 
 // ---------------------------------------------------------------------------
 // crossing bins (bigcount): inserts with stream rank >= 255 - c0 are "full"
-// (ByteStorage::add, storage.hh:590-603).  K-th smallest k-mer index by a
-// 4-pass 8-bit radix select over the bin's records.
-__global__ void __launch_bounds__(256) k_crossing(Params P, const uint64_t *off2, const uint64_t *rec,
-                                                  const uint64_t *cross, const uint64_t *ctr, uint64_t cap_cross,
-                                                  uint8_t *fullf) {
-    __shared__ uint32_t hist[256];
-    __shared__ uint32_t s_sel[2];
-    uint64_t ncross = ctr[CTR_NCROSS];
-    if (ncross > cap_cross) ncross = cap_cross;
-    const uint64_t rmask = (1ull << P.s0) - 1;
-    for (uint64_t c = blockIdx.x; c < ncross; c += gridDim.x) {
-        const uint64_t G = cross[c] >> 8;
-        const uint32_t c0 = (uint32_t)(cross[c] & 0xFF);
-        const uint64_t region = G >> P.s0;
-        const uint32_t o = (uint32_t)(G & rmask);
-        const uint64_t e0 = off2[region], e1 = off2[region + 1];
-        uint32_t K = 255 - c0;          // rank of the first full insert (< the bin's inserts: c0 + n > 255)
-        uint32_t prefix = 0;
-        for (int pass = 0; pass < 4; pass++) {
-            const int sh = 24 - 8 * pass;
-            for (int t = threadIdx.x; t < 256; t += blockDim.x) hist[t] = 0;
+// (ByteStorage::add, storage.hh:590-603).  One workgroup per region with
+// crossings: up to X_GB of its crossing bins at a time get the K-th smallest
+// k-mer index of their records by a 4-pass 8-bit radix select, all of them in
+// the same sweeps over the region's records (LDS slot map offset -> bin).
+constexpr int X_GB = 32;
+__global__ void __launch_bounds__(256) k_crossing(Params P, const uint64_t *rec, const uint4 *xseg,
+                                                  const uint32_t *xent, const uint64_t *ctr, uint8_t *fullf) {
+    __shared__ uint8_t slot[1 << 14];
+    __shared__ uint32_t hist[X_GB * 257];    // padded rows: slot s's serial scan stays on its own banks
+    __shared__ uint32_t s_pre[X_GB], s_k[X_GB];
+    const uint64_t nseg = ctr[CTR_NCROSS];
+    const uint32_t R = 1u << P.s0;
+    for (uint64_t sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
+        const uint4 d = xseg[sg];
+        const uint64_t e0 = (uint64_t)d.x | ((uint64_t)d.y << 32), e1 = e0 + d.z;
+        const uint32_t m = d.w;
+        for (uint32_t g0 = 0; g0 < m; g0 += X_GB) {
+            const uint32_t nb = min((uint32_t)X_GB, m - g0);
+            for (uint32_t x = threadIdx.x; x < R / 4; x += blockDim.x) ((uint32_t *)slot)[x] = 0xFFFFFFFFu;
             block_sync();
+            if (threadIdx.x < nb) {
+                const uint32_t e = xent[e0 + g0 + threadIdx.x];
+                slot[e >> 8] = (uint8_t)threadIdx.x;
+                s_k[threadIdx.x] = 255 - (e & 0xFF);   // rank of the first full insert (< the bin's inserts)
+                s_pre[threadIdx.x] = 0;
+            }
+            block_sync();
+            for (int pass = 0; pass < 4; pass++) {
+                const int sh = 24 - 8 * pass;
+                for (uint32_t x = threadIdx.x; x < nb * 257; x += blockDim.x) hist[x] = 0;
+                block_sync();
+                for (uint64_t q = e0 + threadIdx.x; q < e1; q += blockDim.x) {
+                    const uint64_t v = rec[q];
+                    const uint32_t sl = slot[(uint32_t)v];
+                    if (sl == 0xFF) continue;
+                    const uint32_t j = (uint32_t)(v >> 32);
+                    if (pass > 0 && (j >> (sh + 8)) != (s_pre[sl] >> (sh + 8))) continue;
+                    atomicAdd(&hist[sl * 257 + ((j >> sh) & 0xFF)], 1u);
+                }
+                block_sync();
+                if (threadIdx.x < nb) {
+                    const uint32_t sl = threadIdx.x;
+                    uint32_t K = s_k[sl], acc = 0, dg = 0;
+                    for (dg = 0; dg < 256; dg++) {
+                        const uint32_t h = hist[sl * 257 + dg];
+                        if (acc + h > K) break;
+                        acc += h;
+                    }
+                    s_pre[sl] |= dg << sh;
+                    s_k[sl] = K - acc;
+                }
+                block_sync();
+            }
             for (uint64_t q = e0 + threadIdx.x; q < e1; q += blockDim.x) {
                 const uint64_t v = rec[q];
-                if ((uint32_t)v != o) continue;
+                const uint32_t sl = slot[(uint32_t)v];
+                if (sl == 0xFF) continue;
                 const uint32_t j = (uint32_t)(v >> 32);
-                if (pass > 0 && (j >> (sh + 8)) != (prefix >> (sh + 8))) continue;
-                atomicAdd(&hist[(j >> sh) & 0xFF], 1u);
+                if (j >= s_pre[sl]) full_add(fullf, j);
             }
             block_sync();
-            if (threadIdx.x == 0) {
-                uint32_t acc = 0, d = 0;
-                for (d = 0; d < 256; d++) {
-                    if (acc + hist[d] > K) break;
-                    acc += hist[d];
-                }
-                s_sel[0] = d;
-                s_sel[1] = K - acc;
-            }
-            block_sync();
-            prefix |= s_sel[0] << sh;
-            K = s_sel[1];
-            block_sync();
         }
-        for (uint64_t q = e0 + threadIdx.x; q < e1; q += blockDim.x) {
-            const uint64_t v = rec[q];
-            if ((uint32_t)v != o) continue;
-            const uint32_t j = (uint32_t)(v >> 32);
-            if (j >= prefix) full_add(fullf, j);
-        }
-        block_sync();
     }
 }
 
 // ---------------------------------------------------------------------------
 // finalize (bigcount and/or per-k-mer hash output only): k-mers full in every
-// table feed the bigcount map (16 flags per thread via 16-byte loads)
+// table are bigcount events (storage.hh:606-616), aggregated per hash in an
+// open-addressing device map (one count per distinct hash; the host merges
+// min(65535, base + count), which is order-independent).  A probe run longer
+// than BC_PROBES flags CTR_ERR bit 2: the host grows the map and reruns.
+constexpr int BC_PROBES = 128;
+__device__ __forceinline__ void bc_event(uint64_t *keys, uint32_t *cnt, uint64_t mask, uint64_t *ctr, uint64_t h) {
+    if (h == BC_EMPTY) {
+        atomicAdd((unsigned long long *)&ctr[CTR_BCFF], 1ull);
+        return;
+    }
+    uint64_t s = fmix64(h) & mask;
+    for (int probe = 0; probe < BC_PROBES; probe++, s = (s + 1) & mask) {
+        uint64_t k = __atomic_load_n(&keys[s], __ATOMIC_RELAXED);
+        if (k == BC_EMPTY) {
+            k = atomicCAS((unsigned long long *)&keys[s], (unsigned long long)BC_EMPTY, (unsigned long long)h);
+            if (k == BC_EMPTY) {
+                atomicAdd((unsigned long long *)&ctr[CTR_NBC], 1ull);
+                k = h;
+            }
+        }
+        if (k == h) {
+            atomicAdd(&cnt[s], 1u);
+            return;
+        }
+    }
+    atomicOr((unsigned long long *)&ctr[CTR_ERR], 2ull);
+}
+
 template <class Src>
 __global__ void __launch_bounds__(FIN_THREADS) k_finalize(Params P, Src src, uint64_t nkmers, const uint8_t *fullf,
-                                                         uint64_t *ctr, uint64_t *bc, uint64_t cap_bc,
+                                                         uint64_t *ctr, uint64_t *bck, uint32_t *bcv, uint64_t bmask,
                                                          uint64_t *out_hash) {
-    const bool bigc = P.kind == BYTE && P.use_bigcount;
+    const bool bigc = P.kind == BYTE && P.use_bigcount && bck;
     const uint64_t nchunk = (nkmers + 15) / 16;
     for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nchunk;
          c += (uint64_t)gridDim.x * blockDim.x) {
@@ -698,11 +742,7 @@ __global__ void __launch_bounds__(FIN_THREADS) k_finalize(Params P, Src src, uin
                 const uint8_t *fb = (const uint8_t *)&fv;
                 for (int u = 0; u < 16; u++) {
                     const uint64_t j = c * 16 + u;
-                    if (j < nkmers && fb[u] == (uint8_t)P.n) {
-                        const uint64_t idx = atomicAdd((unsigned long long *)&ctr[CTR_NBC], 1ull);
-                        if (idx < cap_bc) bc[idx] = kmer_hash_global(src, j);
-                        else atomicOr((unsigned long long *)&ctr[CTR_ERR], 2ull);
-                    }
+                    if (j < nkmers && fb[u] == (uint8_t)P.n) bc_event(bck, bcv, bmask, ctr, kmer_hash_global(src, j));
                 }
             }
         }
@@ -712,6 +752,18 @@ __global__ void __launch_bounds__(FIN_THREADS) k_finalize(Params P, Src src, uin
                 if (j < nkmers) out_hash[j] = kmer_hash_global(src, j);
             }
         }
+    }
+}
+
+// occupied map slots -> (keys, counts) for the host merge
+__global__ void k_bc_compact(const uint64_t *bck, const uint32_t *bcv, uint64_t cap, uint64_t *ctr, uint64_t *keys,
+                             uint32_t *cnts) {
+    for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = bck[s];
+        if (k == BC_EMPTY) continue;
+        const uint64_t i = atomicAdd((unsigned long long *)&ctr[CTR_BCOUT], 1ull);
+        keys[i] = k;
+        cnts[i] = bcv[s];
     }
 }
 

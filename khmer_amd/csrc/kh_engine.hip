@@ -80,6 +80,9 @@ static PassGeo pass_geo(const Params &P, uint64_t nkmers) {
     return q;
 }
 
+static void bcmap_alloc(Workspace &w, uint64_t cap);
+static void bcmap_clear(Workspace &w, hipStream_t st);
+
 static void ws_prepare(Graph *g, const PassGeo &q) {
     Workspace &w = g->ws;
     if (q.nkmers > w.cap_kmers) {
@@ -104,18 +107,55 @@ static void ws_prepare(Graph *g, const PassGeo &q) {
         KH_HIP(hipMalloc((void **)&w.off2, (regions + 1) * 8 + 64));
         w.cap_regions = regions;
     }
+    ensure((void **)&w.xseg, &w.cap_xseg, regions + 1, sizeof(uint4));
     if (!w.ctr) {
         KH_HIP(hipMalloc((void **)&w.ctr, CTR_N * 8));
         KH_HIP(hipHostMalloc((void **)&w.h_ctr, CTR_N * 8, hipHostMallocDefault));
     }
-    if (!w.cross) {
-        w.cap_cross = 1 << 20;
-        KH_HIP(hipMalloc((void **)&w.cross, w.cap_cross * 8));
+    if (g->kind == BYTE && g->use_bigcount && !w.bck) bcmap_alloc(w, 1ull << 20);
+}
+
+// ---- per-pass bigcount map (k_finalize) ----
+static void bcmap_alloc(Workspace &w, uint64_t cap) {
+    for (void **pp : {(void **)&w.bck, (void **)&w.bcv, (void **)&w.bc, (void **)&w.bcn})
+        if (*pp) { KH_HIP(hipFree(*pp)); *pp = nullptr; }
+    KH_HIP(hipMalloc((void **)&w.bck, cap * 8));
+    KH_HIP(hipMalloc((void **)&w.bcv, cap * 4));
+    KH_HIP(hipMalloc((void **)&w.bc, cap * 8));
+    KH_HIP(hipMalloc((void **)&w.bcn, cap * 4));
+    w.cap_bcmap = cap;
+}
+
+static void bcmap_clear(Workspace &w, hipStream_t st) {
+    KH_HIP(hipMemsetAsync(w.bck, 0xFF, w.cap_bcmap * 8, st));
+    KH_HIP(hipMemsetAsync(w.bcv, 0, w.cap_bcmap * 4, st));
+}
+
+// ByteStorage::add's bigcount update (storage.hh:606-616) for a whole pass:
+// f full inserts of hash h give bc[h] = min(65535, base + f), base = bc[h] if
+// present else 255 -- the same value as f sequential updates.
+static void bcmap_merge(Graph *g, uint64_t nkeys, uint64_t n_ff) {
+    Workspace &w = g->ws;
+    auto bump = [&](uint64_t h, uint64_t f) {
+        auto it = g->bigcounts.find(h);
+        const uint64_t base = it == g->bigcounts.end() ? 255 : it->second;
+        g->bigcounts[h] = (uint16_t)std::min<uint64_t>(base + f, 65535);
+    };
+    if (n_ff) bump(BC_EMPTY, n_ff);
+    if (nkeys) {
+        const unsigned grid = (unsigned)std::min<uint64_t>((w.cap_bcmap + 255) / 256, 8192);
+        hipLaunchKernelGGL(k_bc_compact, dim3(grid), dim3(256), 0, g->stream, w.bck, w.bcv, w.cap_bcmap, w.ctr, w.bc,
+                           w.bcn);
+        KH_HIP(hipGetLastError());
+        std::vector<uint64_t> keys(nkeys);
+        std::vector<uint32_t> cnts(nkeys);
+        KH_HIP(hipMemcpyAsync(keys.data(), w.bc, nkeys * 8, hipMemcpyDeviceToHost, g->stream));
+        KH_HIP(hipMemcpyAsync(cnts.data(), w.bcn, nkeys * 4, hipMemcpyDeviceToHost, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+        g->bigcounts.reserve(g->bigcounts.size() + nkeys);
+        for (uint64_t i = 0; i < nkeys; i++) bump(keys[i], cnts[i]);
     }
-    if (!w.bc) {
-        w.cap_bc = 1 << 22;
-        KH_HIP(hipMalloc((void **)&w.bc, w.cap_bc * 8));
-    }
+    if (nkeys || n_ff) g->bc_dirty = true;
 }
 
 // record buffers for a pass holding `recs` records (level-1 out / level-2 out;
@@ -422,7 +462,10 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     const uint64_t flag_bytes = (nkmers + 15) & ~15ull;
 
     KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
-    if (bigc) KH_HIP(hipMemsetAsync(w.fullf, 0, flag_bytes, st));
+    if (bigc) {
+        KH_HIP(hipMemsetAsync(w.fullf, 0, flag_bytes, st));
+        bcmap_clear(w, st);
+    }
 
     // level 1
     uint64_t nrec = 0;   // records this pass writes (all on one device; the owned ones on a shard)
@@ -496,8 +539,8 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     A.win = win;
     A.wcnt = w.wcnt;
     A.fullf = w.fullf;
-    A.cross = w.cross;
-    A.cap_cross = w.cap_cross;
+    A.xent = wout;       // free until scatter_w: crossing entries live there meanwhile
+    A.xseg = w.xseg;
     A.ctr = w.ctr;
     A.rprefix[0] = 0;
     for (int i = 0; i < P.n; i++)
@@ -512,8 +555,8 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
         TIMED("apply_byte", hipLaunchKernelGGL(k_apply_count<BYTE>, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P),
                                                st, P, A));
     if (bigc)
-        TIMED("crossing", hipLaunchKernelGGL(k_crossing, dim3(1024), dim3(256), 0, st, P, w.off2, w.rec2, w.cross,
-                                             w.ctr, w.cap_cross, w.fullf));
+        TIMED("crossing", hipLaunchKernelGGL(k_crossing, dim3(1024), dim3(256), 0, st, P, w.rec2, w.xseg, wout,
+                                             w.ctr, w.fullf));
 
     // winners -> k-mer windows
     const size_t wmeta = W_RPC * 8 + (W_RPC + 4) * 4;
@@ -546,13 +589,13 @@ static void pass_stage_c(Graph *g, const Src &src, PassState &ps, const PassOut 
     const uint64_t flag_bytes = (nkmers + 15) & ~15ull;
     uint64_t *d_out_hash = nullptr;
     if (out && out->h_hash) d_out_hash = w.rec2;  // level-2 records are dead after crossing
-    if (bigc || d_out_hash) {
-        const uint64_t nchunk = flag_bytes / 16;
-        const unsigned fgrid = (unsigned)std::max<uint64_t>(
-            1, std::min<uint64_t>((nchunk + FIN_THREADS - 1) / FIN_THREADS, 4096));
+    const uint64_t nchunk = flag_bytes / 16;
+    const unsigned fgrid = (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>((nchunk + FIN_THREADS - 1) / FIN_THREADS, 4096));
+    if (bigc || d_out_hash)
         TIMED("finalize", hipLaunchKernelGGL(k_finalize<Src>, dim3(fgrid), dim3(FIN_THREADS), 0, st, P, src, nkmers,
-                                             w.fullf, w.ctr, w.bc, w.cap_bc, d_out_hash));
-    }
+                                             w.fullf, w.ctr, bigc ? w.bck : nullptr, w.bcv, w.cap_bcmap - 1,
+                                             d_out_hash));
     KH_HIP(hipGetLastError());
     KH_HIP(hipMemcpyAsync(w.h_ctr, w.ctr, CTR_N * 8, hipMemcpyDeviceToHost, st));
     std::vector<uint32_t> hbits;
@@ -565,26 +608,23 @@ static void pass_stage_c(Graph *g, const Src &src, PassState &ps, const PassOut 
     engine_collect_events(g);
     if (want_new)
         for (uint64_t j = 0; j < nkmers; j++) out->h_new[j] = (uint8_t)((hbits[j >> 5] >> (j & 31)) & 1);
-    if (w.h_ctr[CTR_ERR]) fail(KH_EDEVICE, "device overflow of crossing/bigcount buffers");
+    // bigcount map overflow (a probe run too long): grow it and redo the
+    // finalize of this pass (fullf and the source are intact; the map is per pass)
+    while (bigc && (w.h_ctr[CTR_ERR] & 2)) {
+        bcmap_alloc(w, w.cap_bcmap * 4);
+        bcmap_clear(w, st);
+        KH_HIP(hipMemsetAsync(w.ctr + CTR_NBC, 0, 16, st));    // CTR_NBC, CTR_ERR
+        KH_HIP(hipMemsetAsync(w.ctr + CTR_BCFF, 0, 8, st));
+        TIMED("finalize", hipLaunchKernelGGL(k_finalize<Src>, dim3(fgrid), dim3(FIN_THREADS), 0, st, P, src, nkmers,
+                                             w.fullf, w.ctr, w.bck, w.bcv, w.cap_bcmap - 1, (uint64_t *)nullptr));
+        KH_HIP(hipMemcpyAsync(w.h_ctr, w.ctr, CTR_N * 8, hipMemcpyDeviceToHost, st));
+        KH_HIP(hipStreamSynchronize(st));
+        engine_collect_events(g);
+    }
+    if (w.h_ctr[CTR_ERR]) fail(KH_EDEVICE, "device pipeline error flag set");
     g->n_occupied += w.h_ctr[CTR_OCC];
     g->n_unique += w.h_ctr[CTR_UNIQUE];
-    const uint64_t nbc = w.h_ctr[CTR_NBC];
-    if (nbc) {
-        std::vector<uint64_t> hs(nbc);
-        KH_HIP(hipMemcpy(hs.data(), w.bc, nbc * 8, hipMemcpyDeviceToHost));
-        // ByteStorage::add bigcount update (storage.hh:606-616), merged per hash:
-        // absent -> 255 + f, present -> v + f, capped at 65535
-        std::sort(hs.begin(), hs.end());
-        for (uint64_t a = 0; a < nbc;) {
-            uint64_t b = a;
-            while (b < nbc && hs[b] == hs[a]) b++;
-            auto it = g->bigcounts.find(hs[a]);
-            const uint64_t base = it == g->bigcounts.end() ? 255 : it->second;
-            g->bigcounts[hs[a]] = (uint16_t)std::min<uint64_t>(base + (b - a), 65535);
-            a = b;
-        }
-        g->bc_dirty = true;
-    }
+    if (bigc) bcmap_merge(g, w.h_ctr[CTR_NBC], w.h_ctr[CTR_BCFF]);
 }
 
 template <class Src>
@@ -1033,8 +1073,8 @@ Graph::~Graph() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
     Workspace &w = ws;
-    void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.fullf, w.newbits, w.bc, w.off1, w.ch2,
-                    w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.cross, w.ctr, w.d_words, w.d_koff, w.d_bytes,
+    void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.fullf, w.newbits, w.bc, w.bcn, w.bck, w.bcv,
+                    w.off1, w.ch2, w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.xseg, w.ctr, w.d_words, w.d_koff, w.d_bytes,
                     w.q_hashes, w.q_counts, w.frec, w.fcount};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);

@@ -92,7 +92,14 @@ struct Workspace {
     unsigned long long *fcount = nullptr;        // k_own_filter output counter
     uint8_t *fullf = nullptr;                    // per k-mer bigcount "full" tallies
     uint32_t *newbits = nullptr;                 // per k-mer new flags (bitmap)
-    uint64_t *bc = nullptr;                      // bigcount candidate hashes
+    // bigcount events of a pass, aggregated on the device: open-addressing map
+    // hash -> number of "full" inserts (cleared per pass), compacted into
+    // (bc, bcn) for the host merge into Graph::bigcounts
+    uint64_t *bck = nullptr;                     // map keys (BC_EMPTY = free)
+    uint32_t *bcv = nullptr;                     // map counts
+    uint64_t *bc = nullptr;                      // compacted keys
+    uint32_t *bcn = nullptr;                     // compacted counts
+    uint64_t cap_bcmap = 0;                      // map slots (power of two); bc/bcn hold as many
     // partition bookkeeping
     uint64_t *off1 = nullptr;        // [F1+1] level-1 bucket offsets
     uint32_t *ch2 = nullptr;         // [F1+1] level-2 chunk prefix per bucket
@@ -102,10 +109,10 @@ struct Workspace {
     void *scan_tmp = nullptr;        // rocPRIM scan temporary storage
     uint32_t *wcnt = nullptr;        // [regions] winners per region
     uint64_t cap_m = 0, cap_moff = 0, cap_scan = 0, cap_newbits = 0, cap_wcnt = 0;
-    uint64_t *cross = nullptr;       // crossing bins: (global bin << 8) | c0
+    uint4 *xseg = nullptr;           // crossing-bin segments, one per region with crossings
     uint64_t *ctr = nullptr;         // counters, see CTR_*
     uint64_t *h_ctr = nullptr;       // pinned host mirror
-    uint64_t cap_regions = 0, cap_cross = 0, cap_bc = 0;
+    uint64_t cap_regions = 0, cap_xseg = 0;
     // staging for host-fed batches
     uint64_t *d_words = nullptr, *d_koff = nullptr;
     uint8_t *d_bytes = nullptr;
@@ -115,7 +122,8 @@ struct Workspace {
     uint16_t *q_counts = nullptr;
     uint64_t cap_q = 0, cap_q16 = 0;
 };
-enum { CTR_OCC = 0, CTR_UNIQUE, CTR_NCROSS, CTR_NBC, CTR_ERR, CTR_NFULL, CTR_N };
+enum { CTR_OCC = 0, CTR_UNIQUE, CTR_NCROSS, CTR_NBC, CTR_ERR, CTR_NFULL, CTR_BCFF, CTR_BCOUT, CTR_N };
+constexpr uint64_t BC_EMPTY = ~0ull;   // free map slot; events of hash ~0 count in CTR_BCFF
 
 struct Graph {
     int kind = BYTE, hash = TWOBIT, k = 0, n = 0, device = 0;

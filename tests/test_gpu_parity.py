@@ -363,3 +363,30 @@ def test_multibatch_saturated_bigcount(path, batch):
     assert dict(zip(keys, vals)) == o.bigcounts()
     assert len(o.bigcounts()) > 1000
     assert (g.n_unique_kmers(), g.n_occupied()) == (o.n_unique_kmers(), o.n_occupied())
+
+
+@pytest.mark.parametrize("batch", [1 << 27, 1 << 19])
+def test_bigcount_map_growth(batch):
+    """Tiny tables saturate at once, so nearly every k-mer of 2.6M is a
+    bigcount event with its own hash: the per-pass device map must grow past
+    its initial 2^20 slots (and rerun its finalize) and stay exact."""
+    import ctypes
+    from khmer_amd._lib import lib, check
+    sizes = [1009, 1013]
+    g, o = make_pair("Countgraph", 21, sizes, bigcount=True)
+    check(lib.kh_graph_set_batch_kmers(g._g, batch))
+    seqs, offs = synth.batch(0, 20000, 150)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    out = ctypes.c_uint64()
+    check(lib.kh_consume_seqs(g._g, seqs, offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), 20000, 1,
+                              ctypes.byref(out)))
+    assert out.value == o.consume_batch(seqs, [int(v) for v in offs])
+    assert_same(g, o, "bigcount map growth")
+    n = ctypes.c_uint64()
+    check(lib.kh_graph_get_bigcounts(g._g, None, None, 0, ctypes.byref(n)))
+    keys = (ctypes.c_uint64 * n.value)()
+    vals = (ctypes.c_uint16 * n.value)()
+    check(lib.kh_graph_get_bigcounts(g._g, keys, vals, n.value, ctypes.byref(n)))
+    want = o.bigcounts()
+    assert len(want) > (1 << 20)
+    assert dict(zip(keys, vals)) == want
