@@ -21,7 +21,7 @@ constexpr int FIN_THREADS = 256;
 constexpr int W_RPC = 64;              // regions per winner chunk
 
 struct ApplyArgs {
-    const uint64_t *off2;
+    const uint64_t *rlo, *rhi;   // region g's records: [rlo[g], rhi[g])
     const uint64_t *rec;
     uint8_t *tab;
     uint32_t *win;        // winners of region rr at win[e0(rr) ...]
@@ -61,7 +61,7 @@ __device__ __forceinline__ Bounds load_bounds(const Params &P, const ApplyArgs &
     if (rr >= total) return Bounds{0, 0};
     int i;
     const uint64_t region = region_index(P, A, rr, &i);
-    return Bounds{A.off2[region], A.off2[region + 1]};
+    return Bounds{A.rlo[region], A.rhi[region]};
 }
 
 // region rr -> table, bins, record range
@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
             for (uint64_t q = ri.e0 + t; q < ri.e1; q += APPLY_THREADS) {
                 const uint64_t x = A.rec[q];
                 const uint32_t o = (uint32_t)x;
-                if ((full255[o >> 5] >> (o & 31)) & 1) full_add(A.fullf, (uint32_t)(x >> 32));
+                if (x != ~0ull && ((full255[o >> 5] >> (o & 31)) & 1)) full_add(A.fullf, (uint32_t)(x >> 32));
             }
         }
         uint32_t wall;
@@ -666,6 +666,7 @@ __global__ void __launch_bounds__(256) k_crossing(Params P, const uint64_t *rec,
                 block_sync();
                 for (uint64_t q = e0 + threadIdx.x; q < e1; q += blockDim.x) {
                     const uint64_t v = rec[q];
+                    if (v == ~0ull) continue;   // fixed-capacity level 2 sentinel
                     const uint32_t sl = slot[(uint32_t)v];
                     if (sl == 0xFF) continue;
                     const uint32_t j = (uint32_t)(v >> 32);
@@ -688,6 +689,7 @@ __global__ void __launch_bounds__(256) k_crossing(Params P, const uint64_t *rec,
             }
             for (uint64_t q = e0 + threadIdx.x; q < e1; q += blockDim.x) {
                 const uint64_t v = rec[q];
+                if (v == ~0ull) continue;
                 const uint32_t sl = slot[(uint32_t)v];
                 if (sl == 0xFF) continue;
                 const uint32_t j = (uint32_t)(v >> 32);

@@ -181,6 +181,60 @@ static void ensure_recs(Graph *g, uint64_t recs) {
     w.cap_recs = cap;
 }
 
+// ---- fixed-capacity level 2 (k_scatter_l2f) ----
+// Workgroups per level-1 bucket: enough for ~2048 in the grid.
+static uint32_t l2f_parts(uint32_t F1) { return std::max<uint32_t>(1, std::min<uint32_t>(16, (2048 + F1 - 1) / F1)); }
+static size_t lds_scatter_l2f(const Params &P) { return ((size_t)1 << P.s2) * (8 + 8 + 16 * 8 + 4 + 4); }
+
+// The fixed-capacity path is used when a full region expects >= 512 records
+// per pass (the capacity slack is then a few percent); KH_L2_EXACT=1 forces
+// the histogram path (development).
+static bool l2f_wanted(const Graph *g, uint64_t nkmers) {
+    static const bool off = [] { const char *e = getenv("KH_L2_EXACT"); return e && atoi(e); }();
+    if (off || g->l2_cool > 0) return false;
+    const Params &P = g->prm;
+    if ((1u << P.s2) > 1024) return false;
+    for (int i = 0; i < P.n; i++)
+        if ((double)nkmers * (double)(1ull << P.s0) / (double)P.p[i] < 512.0) return false;
+    return true;
+}
+
+// Region capacities for passes of `nkmers` k-mers: expected records (a table
+// gets one record per k-mer, spread over its p_i bins) + 8 sigma + the
+// partially filled blocks of every workgroup; uploaded once per pass size.
+// Returns the total capacity in records.
+static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
+    Workspace &w = g->ws;
+    const Params &P = g->prm;
+    if (w.reg_base && w.reg_nkmers == nkmers) return w.reg_total;
+    const uint64_t nreg = (uint64_t)P.F1 << P.s2;
+    const uint64_t R = 1ull << P.s0;
+    const uint64_t slack = (uint64_t)(l2f_parts(P.F1) + 1) * L2F_BLK + 16;
+    std::vector<uint64_t> base(nreg + 1, 0);
+    uint64_t acc = 0;
+    int i = 0;
+    for (uint64_t gi = 0; gi < nreg; gi++) {
+        base[gi] = acc;
+        const uint64_t lo = gi * R;
+        while (i + 1 < P.n && lo >= P.tbase[i + 1]) i++;
+        if (lo >= P.tbase[i] + P.lsz[i]) continue;   // padding up to the next bucket boundary
+        const uint64_t nb = std::min<uint64_t>(R, P.tbase[i] + P.lsz[i] - lo);
+        const double mean = (double)nkmers * (double)nb / (double)P.p[i];
+        uint64_t c = (uint64_t)(mean + 8.0 * sqrt(mean)) + slack;
+        acc += (c + 15) & ~15ull;
+    }
+    base[nreg] = acc;
+    ensure((void **)&w.reg_base, &w.cap_reg, nreg + 1, 8);
+    uint64_t cap_cur = 0;
+    if (w.reg_cur) KH_HIP(hipFree(w.reg_cur));
+    w.reg_cur = nullptr;
+    ensure((void **)&w.reg_cur, &cap_cur, nreg, 8);
+    KH_HIP(hipMemcpy(w.reg_base, base.data(), (nreg + 1) * 8, hipMemcpyHostToDevice));
+    w.reg_nkmers = nkmers;
+    w.reg_total = acc;
+    return acc;
+}
+
 // KH_CHECK (development): record buffers pre-filled with a sentinel; after
 // each scatter the slots still holding it (holes) are counted
 static bool check_mode() {
@@ -461,6 +515,8 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     }();
     const uint64_t flag_bytes = (nkmers + 15) & ~15ull;
 
+    const bool l2f_try = l2f_wanted(g, nkmers);
+    const uint64_t cap2 = l2f_try ? reg_plan(g, nkmers) : 0;   // level-2 capacity (records)
     KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
     if (bigc) {
         KH_HIP(hipMemsetAsync(w.fullf, 0, flag_bytes, st));
@@ -480,7 +536,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
         TIMED("scan", scan_counts(g, w.mcnt, w.moff, F1 * nch));
         TIMED("plan_l2", hipLaunchKernelGGL(k_plan_l2, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1,
                                             nch, w.moff, w.mcnt, w.off1, w.ch2));
-        ensure_recs(g, nrec);
+        ensure_recs(g, std::max(nrec, cap2));
         if (check_mode()) {
             KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
             KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
@@ -500,7 +556,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                                         w.moff, w.mcnt, w.off1, w.ch2));
     KH_HIP(hipMemcpyAsync(&nrec, w.off1 + F1, 8, hipMemcpyDeviceToHost, st));
     KH_HIP(hipStreamSynchronize(st));
-    ensure_recs(g, nrec);
+    ensure_recs(g, std::max(nrec, cap2));
     if (check_mode()) {
         KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
         KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
@@ -515,25 +571,49 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     }
     }
     if (check_mode()) check_holes(g, w.rec1, nrec, "scatter_l1");
-    // level 2
-    const unsigned g2 = (unsigned)q.nch2max;
-    TIMED("hist_l2", hipLaunchKernelGGL(k_hist_l2, dim3(g2), dim3(PT_THREADS), F2 * 4, st, (uint32_t)F1, P.s0, P.s2,
-                                        w.off1, w.ch2, w.rec1, w.mcnt));
-    TIMED("scan", scan_counts(g, w.mcnt, w.moff, F2 * q.nch2max));
-    TIMED("off2", hipLaunchKernelGGL(k_off2, dim3((unsigned)std::min<uint64_t>((F1 * F2 + 255) / 256, 8192)),
-                                     dim3(256), 0, st, (uint32_t)F1, P.s2, w.off1, w.ch2, w.moff, w.off2));
-    TIMED("scatter_l2", hipLaunchKernelGGL(l2_kernel(), dim3(g2), dim3(PT_THREADS),
-                                           lds_scatter_l2(P), st, (uint32_t)F1, P.s0, P.s2, w.off1, w.ch2, w.moff,
-                                           w.rec1, w.rec2));
-
-    if (check_mode()) check_holes(g, w.rec2, nrec, "scatter_l2");
+    // level 2: fixed-capacity regions (one pass over the level-1 records); the
+    // exact histogram path when a region overflowed or the pass is small
+    bool l2f = l2f_try;
+    if (l2f) {
+        const uint64_t nreg = F1 * F2;
+        const uint32_t parts = l2f_parts((uint32_t)F1);
+        hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)std::min<uint64_t>((nreg + 255) / 256, 4096)), dim3(256), 0, st,
+                           w.reg_base, (unsigned long long *)w.reg_cur, nreg);
+        TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(F1 * parts)),
+                                               dim3(PT_THREADS), lds_scatter_l2f(P), st, (uint32_t)F1, P.s0, P.s2,
+                                               parts, w.off1, w.reg_base, (unsigned long long *)w.reg_cur, w.rec1,
+                                               w.rec2, w.ctr));
+        uint64_t err = 0;
+        KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
+        KH_HIP(hipStreamSynchronize(st));
+        if (err & 4) {   // a region overflowed: exact level 2 for this pass and the next few
+            l2f = false;
+            g->l2_cool = 8;
+            KH_HIP(hipMemsetAsync(w.ctr + CTR_ERR, 0, 8, st));
+        }
+    } else if (g->l2_cool > 0) {
+        g->l2_cool--;
+    }
+    if (!l2f) {
+        const unsigned g2 = (unsigned)q.nch2max;
+        TIMED("hist_l2", hipLaunchKernelGGL(k_hist_l2, dim3(g2), dim3(PT_THREADS), F2 * 4, st, (uint32_t)F1, P.s0,
+                                            P.s2, w.off1, w.ch2, w.rec1, w.mcnt));
+        TIMED("scan", scan_counts(g, w.mcnt, w.moff, F2 * q.nch2max));
+        TIMED("off2", hipLaunchKernelGGL(k_off2, dim3((unsigned)std::min<uint64_t>((F1 * F2 + 255) / 256, 8192)),
+                                         dim3(256), 0, st, (uint32_t)F1, P.s2, w.off1, w.ch2, w.moff, w.off2));
+        TIMED("scatter_l2", hipLaunchKernelGGL(l2_kernel(), dim3(g2), dim3(PT_THREADS),
+                                               lds_scatter_l2(P), st, (uint32_t)F1, P.s0, P.s2, w.off1, w.ch2, w.moff,
+                                               w.rec1, w.rec2));
+        if (check_mode()) check_holes(g, w.rec2, nrec, "scatter_l2");
+    }
     // apply (winner segments -> first half of the dead level-1 buffer)
     uint32_t *win = (uint32_t *)w.rec1;
     uint32_t *wout = win + w.cap_recs;
     ps.win = win;
     ps.wout = wout;
     ApplyArgs &A = ps.A;
-    A.off2 = w.off2;
+    A.rlo = l2f ? w.reg_base : w.off2;
+    A.rhi = l2f ? w.reg_cur : w.off2 + 1;
     A.rec = w.rec2;
     A.tab = g->d_tab;
     A.win = win;
@@ -994,6 +1074,7 @@ static void set_lds_limits() {
     KH_LDS_MAX((k_scatter_l2<PT_THREADS, 4, L2_RPT>));
     KH_LDS_MAX((k_scatter_l2<PT_THREADS, 8, L2_RPT>));
     KH_LDS_MAX((k_scatter_l2<PT_THREADS, 16, L2_RPT>));
+    KH_LDS_MAX((k_scatter_l2f<PT_THREADS, L2_RPT>));
     KH_LDS_MAX((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 1>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 2>));
@@ -1074,7 +1155,7 @@ Graph::~Graph() {
     if (stream) (void)hipStreamSynchronize(stream);
     Workspace &w = ws;
     void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.fullf, w.newbits, w.bc, w.bcn, w.bck, w.bcv,
-                    w.off1, w.ch2, w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.xseg, w.ctr, w.d_words, w.d_koff, w.d_bytes,
+                    w.off1, w.ch2, w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.xseg, w.reg_base, w.reg_cur, w.ctr, w.d_words, w.d_koff, w.d_bytes,
                     w.q_hashes, w.q_counts, w.frec, w.fcount};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);

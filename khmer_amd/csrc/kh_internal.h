@@ -110,6 +110,10 @@ struct Workspace {
     uint32_t *wcnt = nullptr;        // [regions] winners per region
     uint64_t cap_m = 0, cap_moff = 0, cap_scan = 0, cap_newbits = 0, cap_wcnt = 0;
     uint4 *xseg = nullptr;           // crossing-bin segments, one per region with crossings
+    // fixed-capacity level 2 (k_scatter_l2f): region g holds [reg_base[g], reg_cur[g])
+    uint64_t *reg_base = nullptr;    // [regions + 1] capacity prefix for passes of reg_nkmers k-mers
+    uint64_t *reg_cur = nullptr;     // [regions] append cursors
+    uint64_t cap_reg = 0, reg_nkmers = 0, reg_total = 0;
     uint64_t *ctr = nullptr;         // counters, see CTR_*
     uint64_t *h_ctr = nullptr;       // pinned host mirror
     uint64_t cap_regions = 0, cap_xseg = 0;
@@ -147,6 +151,7 @@ struct Graph {
     bool bc_dirty = true;
     std::unordered_set<uint64_t> tags;                  // hashgraph.hh:113 all_tags
     uint64_t batch_kmers = 1ull << 27;
+    int l2_cool = 0;                  // passes left on the exact level 2 after a capacity overflow
     Workspace ws;
     // optional per-kernel HIP-event timing (kh_graph_set_profiling)
     bool profile = false;

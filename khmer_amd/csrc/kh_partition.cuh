@@ -679,4 +679,152 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2(uint32_t F1, int s0, int
     }
 }
 
+// ---------------------------------------------------------------------------
+// Level-2 scatter into fixed-capacity regions: no histogram pass over the
+// level-1 records.  Region g owns [reg_base[g], reg_base[g+1]), sized on the
+// host from its expected record count (+8 sigma and the partial blocks).
+// Workgroup (b, p) takes part p of bucket b's level-1 records and appends to
+// the bucket's regions in blocks of L2F_BLK records: one returning atomic per
+// (region, tile) on reg_cur[g] reserves every block the tile needs, so a
+// block is owned by one workgroup and records keep the register-direct
+// 128-B segment writes of k_scatter_l2 (partial segments wait in LDS tails).
+// After the last tile the rest of each partially filled block is set to the
+// ~0 sentinel that every consumer skips; region g's records are then
+// [reg_base[g], reg_cur[g]).  A reservation past the region's capacity (a
+// skewed input) sets ctr[CTR_ERR] bit 4, writes nothing for that region, and
+// the host redoes the pass's level 2 with the exact histogram path.
+constexpr uint32_t L2F_BLK = 64;
+constexpr uint64_t L2F_DEAD = ~0ull;
+
+template <int THREADS, int RPT>
+__global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, int s2, uint32_t parts,
+                                                         const uint64_t *off1, const uint64_t *reg_base,
+                                                         unsigned long long *reg_cur, const uint64_t *rec_in,
+                                                         uint64_t *rec_out, uint64_t *ctr) {
+    constexpr int TILE = THREADS * RPT;
+    constexpr uint32_t SEG = 16, BLK = L2F_BLK;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t F2 = 1u << s2;
+    uint64_t *bcur = (uint64_t *)smem;              // [F2] base of the partially filled block (DEAD: overflowed)
+    uint64_t *nbase = bcur + F2;                    // [F2] base of the blocks reserved for this tile
+    uint64_t *tail = nbase + F2;                    // [F2*SEG] pending partial segments
+    uint32_t *cnt = (uint32_t *)(tail + F2 * SEG);  // [F2] records appended by this workgroup
+    uint32_t *hist = cnt + F2;                      // [F2] this tile's records
+    const uint32_t b = blockIdx.x / parts, p = blockIdx.x % parts;
+    const uint64_t b0 = off1[b], b1 = off1[b + 1];
+    const uint64_t len = (b1 - b0 + parts - 1) / parts;
+    const uint64_t r0 = min(b1, b0 + (uint64_t)p * len), r1 = min(b1, r0 + len);
+    const uint64_t gb = (uint64_t)b << s2;
+    const uint64_t rmask = (1ull << s0) - 1;
+    for (uint32_t d = threadIdx.x; d < F2; d += THREADS) {
+        bcur[d] = 0;
+        cnt[d] = 0;
+        hist[d] = 0;
+    }
+    // output slot of this workgroup's record number L of region d (this tile)
+    auto phys = [&](uint32_t d, uint32_t L) -> uint64_t {
+        const uint32_t split = (cnt[d] + BLK - 1) & ~(BLK - 1);
+        if (L < split) return bcur[d] == L2F_DEAD ? L2F_DEAD : bcur[d] + (L & (BLK - 1));
+        return nbase[d] == L2F_DEAD ? L2F_DEAD : nbase[d] + (L - split);
+    };
+    uint64_t v[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; q++) {
+        const uint64_t idx = r0 + (uint64_t)q * THREADS + threadIdx.x;
+        v[q] = idx < min(r1, r0 + TILE) ? rec_in[idx] : ~0ull;
+    }
+    const uint32_t ntiles = uniform_u32((uint32_t)((r1 - r0 + TILE - 1) / TILE));
+    for (uint32_t ti = 0; ti < ntiles; ti++) {
+        const uint64_t t0 = r0 + (uint64_t)ti * TILE;
+        const bool last = ti + 1 == ntiles;
+        block_sync();
+        uint32_t rank[RPT];
+        uint64_t x[RPT];
+#pragma unroll
+        for (int q = 0; q < RPT; q++) {
+            x[q] = v[q];
+            if (x[q] != ~0ull) rank[q] = atomicAdd(&hist[(uint32_t)x[q] >> s0], 1u);
+        }
+        {
+            const uint64_t n0 = t0 + TILE, n1 = min(r1, n0 + TILE);
+#pragma unroll
+            for (int q = 0; q < RPT; q++) {
+                const uint64_t idx = n0 + (uint64_t)q * THREADS + threadIdx.x;
+                v[q] = idx < n1 ? rec_in[idx] : ~0ull;
+            }
+        }
+        block_sync();
+        // blocks for this tile: one reservation per region that needs any
+        for (uint32_t d = threadIdx.x; d < F2; d += THREADS) {
+            const uint32_t h = hist[d], c0 = cnt[d];
+            uint64_t nb = 0;
+            if (h) {
+                const uint32_t need = (c0 + h + BLK - 1) / BLK - (c0 + BLK - 1) / BLK;
+                if (bcur[d] == L2F_DEAD) {
+                    nb = L2F_DEAD;
+                } else if (need) {
+                    nb = atomicAdd(&reg_cur[gb + d], (unsigned long long)need * BLK);
+                    if (nb + (uint64_t)need * BLK > reg_base[gb + d + 1]) {
+                        atomicOr((unsigned long long *)&ctr[CTR_ERR], 4ull);
+                        nb = L2F_DEAD;
+                    }
+                }
+            }
+            nbase[d] = nb;
+        }
+        block_sync();
+        // pending tails whose segment completes in this tile (all of them on the last tile)
+#pragma unroll 4
+        for (uint32_t y = threadIdx.x; y < F2 * SEG; y += THREADS) {
+            const uint32_t d = y / SEG, sl = y % SEG;
+            const uint32_t c0 = cnt[d], a = c0 & ~(SEG - 1);
+            if (c0 == a || sl >= c0 - a) continue;
+            const uint32_t e = c0 + hist[d];
+            if ((last ? e : (e & ~(SEG - 1))) <= a) continue;
+            const uint64_t pos = phys(d, a + sl);
+            if (pos != L2F_DEAD) rec_out[pos] = tail[y];
+        }
+        block_sync();   // the flushed tail slots are refilled below
+#pragma unroll
+        for (int q = 0; q < RPT; q++) {
+            if (x[q] == ~0ull) continue;
+            const uint32_t d = (uint32_t)x[q] >> s0;
+            const uint32_t L = cnt[d] + rank[q];
+            const uint32_t e = cnt[d] + hist[d];
+            const uint64_t val = (x[q] & ~0xFFFFFFFFull) | (x[q] & rmask);
+            if (L < (last ? e : (e & ~(SEG - 1)))) {
+                const uint64_t pos = phys(d, L);
+                if (pos != L2F_DEAD) rec_out[pos] = val;
+            } else {
+                tail[d * SEG + (L & (SEG - 1))] = val;
+            }
+        }
+        block_sync();
+        for (uint32_t d = threadIdx.x; d < F2; d += THREADS) {
+            const uint32_t h = hist[d];
+            if (!h) continue;
+            const uint32_t c0 = cnt[d];
+            const uint32_t need = (c0 + h + BLK - 1) / BLK - (c0 + BLK - 1) / BLK;
+            if (nbase[d] == L2F_DEAD) bcur[d] = L2F_DEAD;
+            else if (need) bcur[d] = nbase[d] + (uint64_t)(need - 1) * BLK;
+            cnt[d] = c0 + h;
+            hist[d] = 0;
+        }
+    }
+    // the rest of every partially filled block: sentinels
+    block_sync();
+    for (uint32_t y = threadIdx.x; y < F2 * BLK; y += THREADS) {
+        const uint32_t d = y / BLK, sl = y % BLK;
+        const uint32_t c = cnt[d] & (BLK - 1);
+        if (c == 0 || sl < c || bcur[d] == L2F_DEAD) continue;
+        rec_out[bcur[d] + sl] = ~0ull;
+    }
+}
+
+// per-pass region cursors start at their region bases
+__global__ void k_reg_reset(const uint64_t *reg_base, unsigned long long *reg_cur, uint64_t n) {
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x)
+        reg_cur[g] = reg_base[g];
+}
+
 }  // namespace kh
