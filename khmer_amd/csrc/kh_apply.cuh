@@ -85,7 +85,7 @@ struct Prefetch {
     uint64_t v[APPLY_RECS];     // this thread's first records
 };
 
-template <int KIND>
+template <int KIND, int TH = APPLY_THREADS>
 __device__ __forceinline__ void prefetch_region(const Params &P, const ApplyArgs &A, uint64_t rr, uint64_t total,
                                                 Bounds b, Prefetch &f) {
     // every field is written on every path (keeps the struct in registers)
@@ -108,7 +108,7 @@ __device__ __forceinline__ void prefetch_region(const Params &P, const ApplyArgs
     }
 #pragma unroll
     for (int u = 0; u < APPLY_RECS; u++) {
-        const uint64_t q = f.ri.e0 + (uint64_t)u * APPLY_THREADS + t;
+        const uint64_t q = f.ri.e0 + (uint64_t)u * TH + t;
         f.v[u] = q < f.ri.e1 ? A.rec[q] : ~0ull;
     }
 }
@@ -153,10 +153,12 @@ __device__ __forceinline__ uint64_t winner_base(const uint32_t *s_wt, uint32_t *
 
 // Byte (KIND == BYTE) and Nibble storage: ByteStorage::add / NibbleStorage::add
 // (storage.hh:571-624 / 320-359) applied as a batch
-template <int KIND>
-__global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, ApplyArgs A) {
+// TH threads, 16 bins per thread: regions of 2^13 (512 threads) or 2^14 bins
+// (1024 threads) -- one kernel body for both
+template <int KIND, int TH>
+__global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int BPT = 16;               // 2^13 bins / 512 threads
+    constexpr int BPT = 16;               // bins per thread: R == 16 * TH
     const uint32_t R = 1u << P.s0;
     uint32_t *cnt = (uint32_t *)smem;     // [R]
     uint32_t *minj = cnt + R;             // [R]
@@ -172,7 +174,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
     uint64_t occ = 0;
     const uint64_t total = A.rprefix[P.n];
     Prefetch cur, nxt;
-    prefetch_region<KIND>(P, A, blockIdx.x, total, load_bounds(P, A, blockIdx.x, total), cur);
+    prefetch_region<KIND, TH>(P, A, blockIdx.x, total, load_bounds(P, A, blockIdx.x, total), cur);
     Bounds bnext = load_bounds(P, A, blockIdx.x + gridDim.x, total);
 #ifdef KH_PHASES
     uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
@@ -185,7 +187,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
         const RegionInfo ri = cur.ri;
         if (ri.e0 == ri.e1) {
             if (t == 0) A.wcnt[rr] = 0;
-            prefetch_region<KIND>(P, A, rr + gridDim.x, total, bnext, cur);
+            prefetch_region<KIND, TH>(P, A, rr + gridDim.x, total, bnext, cur);
             bnext = load_bounds(P, A, rr + 2 * (uint64_t)gridDim.x, total);
             continue;
         }
@@ -229,12 +231,12 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
         if (!(P.ablate & 2)) {
             // two batches of APPLY_RECS loads in flight: batch k+1 is issued
             // before batch k's atomics, so each wait is for the older batch only
-            const uint64_t step = (uint64_t)APPLY_RECS * APPLY_THREADS;
+            const uint64_t step = (uint64_t)APPLY_RECS * TH;
             uint64_t va[APPLY_RECS], vb[APPLY_RECS];
             uint64_t q0 = ri.e0 + step + t;
 #pragma unroll
             for (int u = 0; u < APPLY_RECS; u++) {
-                const uint64_t q = q0 + (uint64_t)u * APPLY_THREADS;
+                const uint64_t q = q0 + (uint64_t)u * TH;
                 va[u] = q < ri.e1 ? A.rec[q] : ~0ull;
             }
 #pragma unroll
@@ -242,14 +244,14 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
             for (; q0 < ri.e1; q0 += 2 * step) {
 #pragma unroll
                 for (int u = 0; u < APPLY_RECS; u++) {
-                    const uint64_t q = q0 + step + (uint64_t)u * APPLY_THREADS;
+                    const uint64_t q = q0 + step + (uint64_t)u * TH;
                     vb[u] = q < ri.e1 ? A.rec[q] : ~0ull;
                 }
 #pragma unroll
                 for (int u = 0; u < APPLY_RECS; u++) count_record(va[u], cnt, minj);
 #pragma unroll
                 for (int u = 0; u < APPLY_RECS; u++) {
-                    const uint64_t q = q0 + 2 * step + (uint64_t)u * APPLY_THREADS;
+                    const uint64_t q = q0 + 2 * step + (uint64_t)u * TH;
                     va[u] = q < ri.e1 ? A.rec[q] : ~0ull;
                 }
 #pragma unroll
@@ -270,7 +272,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
         const uint32_t lane = t & 63;
 #pragma unroll
         for (int step = 0; step < BPT / 4; step++) {
-            const uint32_t g = t + (uint32_t)step * APPLY_THREADS;   // 4-bin group
+            const uint32_t g = t + (uint32_t)step * TH;   // 4-bin group
             const uint32_t o = 4 * g;
             const uint4 n4 = ((const uint4 *)cnt)[g];
             const uint32_t cw = ((const uint32_t *)c0)[g];
@@ -331,7 +333,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
             const uint64_t seg = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
             A.xseg[seg] = make_uint4((uint32_t)ri.e0, (uint32_t)(ri.e0 >> 32), (uint32_t)(ri.e1 - ri.e0), s_flag[1]);
         }
-        prefetch_region<KIND>(P, A, rr + gridDim.x, total, bnext, nxt);
+        prefetch_region<KIND, TH>(P, A, rr + gridDim.x, total, bnext, nxt);
         bnext = bafter;
         // pass 2: write back changed 16-bin chunks; winners to the region's segment
         for (uint32_t x = t; x < nchunk; x += blockDim.x) {
@@ -359,7 +361,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
             // bins at 255 before the batch: every insert is "full"
             // (ByteStorage::add, storage.hh:590-603); rare, so the region's
             // records are read again
-            for (uint64_t q = ri.e0 + t; q < ri.e1; q += APPLY_THREADS) {
+            for (uint64_t q = ri.e0 + t; q < ri.e1; q += TH) {
                 const uint64_t x = A.rec[q];
                 const uint32_t o = (uint32_t)x;
                 if (x != ~0ull && ((full255[o >> 5] >> (o & 31)) & 1)) full_add(A.fullf, (uint32_t)(x >> 32));
@@ -370,7 +372,7 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_count(Params P, Appl
         if (nw) {
 #pragma unroll
             for (int step = 0; step < BPT / 4; step++) {
-                const uint32_t g = t + (uint32_t)step * APPLY_THREADS;
+                const uint32_t g = t + (uint32_t)step * TH;
                 const uint32_t win = wflag[g];
                 if (!win) continue;
                 const uint4 m = ((const uint4 *)minj)[g];

@@ -235,6 +235,88 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
     return acc;
 }
 
+// ---- fixed-capacity level 1 (k_scatter_l1f) ----
+// up to 1024 buckets (the per-bucket LDS state), hashed sources with <= 8
+// tables per launch; not for shards using the owned-record filter
+static int env_seg(const char *name, int dflt) {   // development: KH_L2_SEG / KH_W_SEG tail sizes
+    const char *e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+static bool use_own_filter(const Graph *g);
+static size_t lds_window(bool window, int tile_kmers);
+static bool l1f_ok(const Graph *g) {
+    static const bool off = [] { const char *e = getenv("KH_L1_EXACT"); return e && atoi(e); }();
+    return !off && g->prm.F1 <= 1024 && !use_own_filter(g);
+}
+static uint32_t device_cus(const Graph *g) {
+    static int cus[64] = {0};
+    const int d = g->device & 63;
+    if (!cus[d]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || v <= 0) v = 256;
+        cus[d] = v;
+    }
+    return (uint32_t)cus[d];
+}
+// a persistent grid: two workgroups per CU (the kernel's LDS allows two at up
+// to ~512 buckets), fewer for small passes
+static uint32_t l1f_wpc() { static const int v = env_seg("KH_L1F_WPC", 2); return (uint32_t)std::max(1, v); }
+static uint32_t l1f_workgroups(const Graph *g, uint64_t nkmers) {
+    const uint64_t tiles = (nkmers + L1_THREADS - 1) / L1_THREADS;
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles / 8 + 1, (uint64_t)l1f_wpc() * device_cus(g)));
+}
+static size_t lds_scatter_l1f(const Params &P, bool window, int tile_kmers) {
+    const size_t F1a = (P.F1 + 3) & ~3u;
+    const size_t tile = (size_t)L1_THREADS * L1_MAX_RPT;
+    return F1a * 8 * 5 + tile * 8 + F1a * 4 * 5 + tile * 2 + 64 + lds_window(window, tile_kmers);
+}
+template <class Src>
+using L1FFn = void (*)(Params, Src, uint64_t, uint64_t, int, int, const uint64_t *, unsigned long long *, uint64_t *,
+                       uint64_t *);
+template <class Src>
+static L1FFn<Src> l1f_kernel(int kpt) {
+    switch (kpt) {
+        case 1: return k_scatter_l1f<Src, 1>;
+        case 2: return k_scatter_l1f<Src, 2>;
+        case 4: return k_scatter_l1f<Src, 4>;
+        default: return k_scatter_l1f<Src, 8>;
+    }
+}
+
+// Bucket capacities for passes of `nkmers` k-mers: expected records + 8 sigma
+// + one partial block per workgroup.  Returns the total capacity in records.
+static uint64_t bkt_plan(Graph *g, uint64_t nkmers) {
+    Workspace &w = g->ws;
+    const Params &P = g->prm;
+    if (w.bkt_base && w.bkt_nkmers == nkmers) return w.bkt_total;
+    const uint64_t F1 = P.F1, span = 1ull << (P.s0 + P.s2);
+    const uint64_t slack = (uint64_t)l1f_workgroups(g, nkmers) * L1F_BLK + 16;
+    std::vector<uint64_t> base(F1 + 1, 0);
+    uint64_t acc = 0;
+    int i = 0;
+    for (uint64_t b = 0; b < F1; b++) {
+        base[b] = acc;
+        const uint64_t lo = b * span;
+        while (i + 1 < P.n && lo >= P.tbase[i + 1]) i++;
+        if (lo >= P.tbase[i] + P.lsz[i]) continue;
+        const uint64_t nb = std::min<uint64_t>(span, P.tbase[i] + P.lsz[i] - lo);
+        const double mean = (double)nkmers * (double)nb / (double)P.p[i];
+        const uint64_t c = (uint64_t)(mean + 8.0 * sqrt(mean)) + slack;
+        acc += (c + 15) & ~15ull;
+    }
+    base[F1] = acc;
+    uint64_t cap = 0;
+    for (void **pp : {(void **)&w.bkt_base, (void **)&w.bkt_cur})
+        if (*pp) { KH_HIP(hipFree(*pp)); *pp = nullptr; }
+    ensure((void **)&w.bkt_base, &cap, F1 + 1, 8);
+    cap = 0;
+    ensure((void **)&w.bkt_cur, &cap, F1 + 1, 8);
+    KH_HIP(hipMemcpy(w.bkt_base, base.data(), (F1 + 1) * 8, hipMemcpyHostToDevice));
+    w.bkt_nkmers = nkmers;
+    w.bkt_total = acc;
+    return acc;
+}
+
 // KH_CHECK (development): record buffers pre-filled with a sentinel; after
 // each scatter the slots still holding it (holes) are counted
 static bool check_mode() {
@@ -388,10 +470,6 @@ static size_t lds_scatter_l1(const Params &P, bool window, int tile_kmers) {
 
 constexpr int L2_SEG = 16;   // 128-B level-2 write segments
 constexpr int L2_RPT = 8;    // level-2 records per thread per tile
-static int env_seg(const char *name, int dflt) {   // development: KH_L2_SEG / KH_W_SEG tail sizes
-    const char *e = getenv(name);
-    return e && *e ? atoi(e) : dflt;
-}
 static int l2_seg() { return env_seg("KH_L2_SEG", L2_SEG); }
 static int w_seg() { return env_seg("KH_W_SEG", 2); }   // measured: 8 -> 26.8, 2 -> 25.5 ms/step
 static size_t lds_scatter_l2(const Params &P) {
@@ -419,6 +497,16 @@ static WFn w_kernel() {
 static size_t lds_scatter_w(uint32_t FJ) {
     const size_t FJa = (FJ + 3) & ~3u;
     return W_RPC * 8 + (W_RPC + 4) * 4 + FJa * 8 + (size_t)PT_TILE * 4 + FJa * 4 * w_seg() + FJa * 4 * 2 + 64 + FJa;
+}
+static int apply_count_threads(const Params &P) { return (1 << P.s0) / 16; }
+template <int KIND>
+static void (*apply_count_kernel(const Params &P))(Params, ApplyArgs) {
+    return P.s0 == 14 ? k_apply_count<KIND, 1024> : k_apply_count<KIND, 512>;
+}
+// one 1024-thread workgroup per CU fits the 2^14-bin LDS footprint; two of 512
+static unsigned agrid_count(const Graph *g, const PassGeo &q) {
+    const uint64_t per_cu = g->prm.s0 == 14 ? 1 : 2;
+    return (unsigned)std::min<uint64_t>(q.regions, per_cu * device_cus(g));
 }
 static size_t lds_apply(const Params &P) {
     const size_t R = (size_t)1 << P.s0;
@@ -523,89 +611,116 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
         bcmap_clear(w, st);
     }
 
-    // level 1
-    uint64_t nrec = 0;   // records this pass writes (all on one device; the owned ones on a shard)
-    if (use_own_filter(g)) {
-        nrec = own_filter(g, src, nkmers, window);
-        const uint32_t nch = (uint32_t)std::max<uint64_t>(1, (nrec + L2_CHUNK - 1) / L2_CHUNK);
-        ensure((void **)&w.mcnt, &w.cap_m, F1 * nch, 4);
-        ensure((void **)&w.moff, &w.cap_moff, F1 * nch, 8);
-        const int shift = P.s0 + P.s2;
-        TIMED("hist_rec", hipLaunchKernelGGL(k_hist_rec, dim3(nch), dim3(PT_THREADS), F1 * 4, st, w.frec, nrec,
-                                             (uint32_t)F1, shift, nch, w.mcnt));
-        TIMED("scan", scan_counts(g, w.mcnt, w.moff, F1 * nch));
-        TIMED("plan_l2", hipLaunchKernelGGL(k_plan_l2, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1,
-                                            nch, w.moff, w.mcnt, w.off1, w.ch2));
-        ensure_recs(g, std::max(nrec, cap2));
-        if (check_mode()) {
-            KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
-            KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
+    // Partition: the fast path hashes every k-mer once into fixed-capacity
+    // level-1 buckets (k_scatter_l1f) and makes one pass over them into
+    // fixed-capacity level-2 regions (k_scatter_l2f); the exact path counts
+    // first (histogram + scan) at both levels.  Capacities hold for any input
+    // that is not heavily skewed; an overflow redoes the pass exactly (the
+    // tables are untouched until apply) and keeps the next few passes exact.
+    bool fast = l2f_try;
+    bool l1f = false;
+    uint64_t nrec = 0;   // records this pass writes (exact level 1 only)
+    for (;;) {
+        l1f = fast && l1f_ok(g);
+        const uint64_t cap1 = l1f ? bkt_plan(g, nkmers) : 0;
+        // level 1
+        if (l1f) {
+            ensure_recs(g, std::max(cap1, cap2));
+            hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)((F1 + 255) / 256)), dim3(256), 0, st, w.bkt_base,
+                               (unsigned long long *)w.bkt_cur, (uint64_t)F1);
+            const uint32_t nwg = l1f_workgroups(g, nkmers);
+            for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
+                const int nt = std::min(L1_MAX_RPT, P.n - t0);
+                const int kpt = std::max(1, L1_MAX_RPT / nt);
+                const uint64_t tk = (uint64_t)L1_THREADS * kpt;
+                const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
+                TIMED("scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt), dim3(nwg), dim3(L1_THREADS),
+                                                       lds_scatter_l1f(P, window, (int)tk), st, P, src, nkmers, kpw,
+                                                       t0, nt, w.bkt_base, (unsigned long long *)w.bkt_cur, w.rec1,
+                                                       w.ctr));
+            }
+        } else if (use_own_filter(g)) {
+            nrec = own_filter(g, src, nkmers, window);
+            const uint32_t nch = (uint32_t)std::max<uint64_t>(1, (nrec + L2_CHUNK - 1) / L2_CHUNK);
+            ensure((void **)&w.mcnt, &w.cap_m, F1 * nch, 4);
+            ensure((void **)&w.moff, &w.cap_moff, F1 * nch, 8);
+            const int shift = P.s0 + P.s2;
+            TIMED("hist_rec", hipLaunchKernelGGL(k_hist_rec, dim3(nch), dim3(PT_THREADS), F1 * 4, st, w.frec, nrec,
+                                                 (uint32_t)F1, shift, nch, w.mcnt));
+            TIMED("scan", scan_counts(g, w.mcnt, w.moff, F1 * nch));
+            TIMED("plan_l2", hipLaunchKernelGGL(k_plan_l2, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1,
+                                                nch, w.moff, w.mcnt, w.off1, w.ch2));
+            ensure_recs(g, std::max(nrec, cap2));
+            if (check_mode()) {
+                KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
+                KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
+            }
+            SrcHashes rs{};
+            rs.h = w.frec;
+            rs.k = P.k;
+            TIMED("scatter_l1", hipLaunchKernelGGL((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>),
+                                                   dim3(nch), dim3(L1_THREADS),
+                                                   lds_scatter_l1(P, false, L1_THREADS * L1_MAX_RPT), st, P, rs, nrec,
+                                                   (uint32_t)L2_CHUNK, nch, 0, 1, w.moff, w.rec1));
+        } else {
+            TIMED("hist_l1", hipLaunchKernelGGL(k_hist_l1<Src>, dim3(q.nch1), dim3(L1_THREADS), lds_hist_l1(P, window),
+                                                st, P, src, nkmers, q.ck1, q.nch1, w.mcnt));
+            TIMED("scan", scan_counts(g, w.mcnt, w.moff, F1 * q.nch1));
+            TIMED("plan_l2", hipLaunchKernelGGL(k_plan_l2, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1,
+                                                q.nch1, w.moff, w.mcnt, w.off1, w.ch2));
+            KH_HIP(hipMemcpyAsync(&nrec, w.off1 + F1, 8, hipMemcpyDeviceToHost, st));
+            KH_HIP(hipStreamSynchronize(st));
+            ensure_recs(g, std::max(nrec, cap2));
+            if (check_mode()) {
+                KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
+                KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
+            }
+            for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
+                const int nt = std::min(L1_MAX_RPT, P.n - t0);
+                const int kpt = std::max(1, L1_MAX_RPT / nt);
+                const int tile_kmers = L1_THREADS * kpt;
+                TIMED("scatter_l1", hipLaunchKernelGGL(l1_kernel<Src>(l1_seg(P) != 0, kpt), dim3(q.nch1),
+                                                       dim3(L1_THREADS), lds_scatter_l1(P, window, tile_kmers), st, P,
+                                                       src, nkmers, q.ck1, q.nch1, t0, nt, w.moff, w.rec1));
+            }
         }
-        SrcHashes rs{};
-        rs.h = w.frec;
-        rs.k = P.k;
-        TIMED("scatter_l1", hipLaunchKernelGGL((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>),
-                                               dim3(nch), dim3(L1_THREADS),
-                                               lds_scatter_l1(P, false, L1_THREADS * L1_MAX_RPT), st, P, rs, nrec,
-                                               (uint32_t)L2_CHUNK, nch, 0, 1, w.moff, w.rec1));
-    } else {
-    TIMED("hist_l1", hipLaunchKernelGGL(k_hist_l1<Src>, dim3(q.nch1), dim3(L1_THREADS), lds_hist_l1(P, window), st, P,
-                                        src, nkmers, q.ck1, q.nch1, w.mcnt));
-    TIMED("scan", scan_counts(g, w.mcnt, w.moff, F1 * q.nch1));
-    TIMED("plan_l2", hipLaunchKernelGGL(k_plan_l2, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1, q.nch1,
-                                        w.moff, w.mcnt, w.off1, w.ch2));
-    KH_HIP(hipMemcpyAsync(&nrec, w.off1 + F1, 8, hipMemcpyDeviceToHost, st));
-    KH_HIP(hipStreamSynchronize(st));
-    ensure_recs(g, std::max(nrec, cap2));
-    if (check_mode()) {
-        KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
-        KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
-    }
-    for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
-        const int nt = std::min(L1_MAX_RPT, P.n - t0);
-        const int kpt = std::max(1, L1_MAX_RPT / nt);
-        const int tile_kmers = L1_THREADS * kpt;
-        TIMED("scatter_l1", hipLaunchKernelGGL(l1_kernel<Src>(l1_seg(P) != 0, kpt), dim3(q.nch1), dim3(L1_THREADS),
-                                               lds_scatter_l1(P, window, tile_kmers), st, P, src, nkmers, q.ck1,
-                                               q.nch1, t0, nt, w.moff, w.rec1));
-    }
-    }
-    if (check_mode()) check_holes(g, w.rec1, nrec, "scatter_l1");
-    // level 2: fixed-capacity regions (one pass over the level-1 records); the
-    // exact histogram path when a region overflowed or the pass is small
-    bool l2f = l2f_try;
-    if (l2f) {
-        const uint64_t nreg = F1 * F2;
-        const uint32_t parts = l2f_parts((uint32_t)F1);
-        hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)std::min<uint64_t>((nreg + 255) / 256, 4096)), dim3(256), 0, st,
-                           w.reg_base, (unsigned long long *)w.reg_cur, nreg);
-        TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(F1 * parts)),
-                                               dim3(PT_THREADS), lds_scatter_l2f(P), st, (uint32_t)F1, P.s0, P.s2,
-                                               parts, w.off1, w.reg_base, (unsigned long long *)w.reg_cur, w.rec1,
-                                               w.rec2, w.ctr));
-        uint64_t err = 0;
-        KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
-        KH_HIP(hipStreamSynchronize(st));
-        if (err & 4) {   // a region overflowed: exact level 2 for this pass and the next few
-            l2f = false;
-            g->l2_cool = 8;
-            KH_HIP(hipMemsetAsync(w.ctr + CTR_ERR, 0, 8, st));
+        if (check_mode() && !l1f) check_holes(g, w.rec1, nrec, "scatter_l1");
+        // level 2
+        if (fast) {
+            const uint64_t nreg = F1 * F2;
+            const uint32_t parts = l2f_parts((uint32_t)F1);
+            hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)std::min<uint64_t>((nreg + 255) / 256, 4096)), dim3(256), 0,
+                               st, w.reg_base, (unsigned long long *)w.reg_cur, nreg);
+            const uint64_t *bs = l1f ? w.bkt_base : w.off1;
+            const uint64_t *be = l1f ? w.bkt_cur : w.off1 + 1;
+            TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(F1 * parts)),
+                                                   dim3(PT_THREADS), lds_scatter_l2f(P), st, (uint32_t)F1, P.s0, P.s2,
+                                                   parts, bs, be, w.reg_base, (unsigned long long *)w.reg_cur, w.rec1,
+                                                   w.rec2, w.ctr));
+            uint64_t err = 0;
+            KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
+            KH_HIP(hipStreamSynchronize(st));
+            if (err & 12) {   // a bucket or region overflowed: redo the pass exactly
+                fast = false;
+                g->l2_cool = 8;
+                KH_HIP(hipMemsetAsync(w.ctr + CTR_ERR, 0, 8, st));
+                continue;
+            }
+        } else {
+            if (g->l2_cool > 0) g->l2_cool--;
+            const unsigned g2 = (unsigned)q.nch2max;
+            TIMED("hist_l2", hipLaunchKernelGGL(k_hist_l2, dim3(g2), dim3(PT_THREADS), F2 * 4, st, (uint32_t)F1, P.s0,
+                                                P.s2, w.off1, w.ch2, w.rec1, w.mcnt));
+            TIMED("scan", scan_counts(g, w.mcnt, w.moff, F2 * q.nch2max));
+            TIMED("off2", hipLaunchKernelGGL(k_off2, dim3((unsigned)std::min<uint64_t>((F1 * F2 + 255) / 256, 8192)),
+                                             dim3(256), 0, st, (uint32_t)F1, P.s2, w.off1, w.ch2, w.moff, w.off2));
+            TIMED("scatter_l2", hipLaunchKernelGGL(l2_kernel(), dim3(g2), dim3(PT_THREADS), lds_scatter_l2(P), st,
+                                                   (uint32_t)F1, P.s0, P.s2, w.off1, w.ch2, w.moff, w.rec1, w.rec2));
+            if (check_mode()) check_holes(g, w.rec2, nrec, "scatter_l2");
         }
-    } else if (g->l2_cool > 0) {
-        g->l2_cool--;
+        break;
     }
-    if (!l2f) {
-        const unsigned g2 = (unsigned)q.nch2max;
-        TIMED("hist_l2", hipLaunchKernelGGL(k_hist_l2, dim3(g2), dim3(PT_THREADS), F2 * 4, st, (uint32_t)F1, P.s0,
-                                            P.s2, w.off1, w.ch2, w.rec1, w.mcnt));
-        TIMED("scan", scan_counts(g, w.mcnt, w.moff, F2 * q.nch2max));
-        TIMED("off2", hipLaunchKernelGGL(k_off2, dim3((unsigned)std::min<uint64_t>((F1 * F2 + 255) / 256, 8192)),
-                                         dim3(256), 0, st, (uint32_t)F1, P.s2, w.off1, w.ch2, w.moff, w.off2));
-        TIMED("scatter_l2", hipLaunchKernelGGL(l2_kernel(), dim3(g2), dim3(PT_THREADS),
-                                               lds_scatter_l2(P), st, (uint32_t)F1, P.s0, P.s2, w.off1, w.ch2, w.moff,
-                                               w.rec1, w.rec2));
-        if (check_mode()) check_holes(g, w.rec2, nrec, "scatter_l2");
-    }
+    const bool l2f = fast;
     // apply (winner segments -> first half of the dead level-1 buffer)
     uint32_t *win = (uint32_t *)w.rec1;
     uint32_t *wout = win + w.cap_recs;
@@ -629,11 +744,11 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     if (P.kind == BIT)
         TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P), st, P, A));
     else if (P.kind == NIBBLE)
-        TIMED("apply_nibble", hipLaunchKernelGGL(k_apply_count<NIBBLE>, dim3(agrid), dim3(APPLY_THREADS),
-                                                 lds_apply(P), st, P, A));
+        TIMED("apply_nibble", hipLaunchKernelGGL(apply_count_kernel<NIBBLE>(P), dim3(agrid_count(g, q)),
+                                                 dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
     else
-        TIMED("apply_byte", hipLaunchKernelGGL(k_apply_count<BYTE>, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P),
-                                               st, P, A));
+        TIMED("apply_byte", hipLaunchKernelGGL(apply_count_kernel<BYTE>(P), dim3(agrid_count(g, q)),
+                                               dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
     if (bigc)
         TIMED("crossing", hipLaunchKernelGGL(k_crossing, dim3(1024), dim3(256), 0, st, P, w.rec2, w.xseg, wout,
                                              w.ctr, w.fullf));
@@ -1022,7 +1137,10 @@ void graph_prepare_params(Graph *g) {
     // ablation studies only
     const char *ab = getenv("KH_ABLATE");
     P.ablate = ab ? atoi(ab) : 0;
-    P.s0 = g->kind == BIT ? 14 : 13;
+    // regions of 2^14 bins (Byte/Nibble: 1024-thread apply, ~154 KiB of LDS;
+    // KH_S0=13 selects the 2^13-bin, 512-thread variant)
+    static const int s0_env = env_seg("KH_S0", 14);
+    P.s0 = g->kind == BIT ? 14 : (s0_env == 13 ? 13 : 14);
     // regions per level-1 bucket: about sqrt(total regions), so both levels
     // fan out to a few hundred destinations (few same-address LDS atomics in
     // the tile ranks), at most 1024 (C2 on one device: 477 x 1024; a shard of
@@ -1034,7 +1152,7 @@ void graph_prepare_params(Graph *g) {
         nreg += r;
     }
     const int half = (ceil_log2(std::max<uint64_t>(nreg, 1)) + 1) / 2;
-    P.s2 = std::min({10, ceil_log2(maxreg), std::max(half, 1)});
+    P.s2 = std::min({10, ceil_log2(maxreg), std::max(half + 1, 1)});
     const uint64_t span = 1ull << (P.s0 + P.s2);
     uint64_t base = 0, byteoff = 0;
     for (int i = 0; i < g->n; i++) {
@@ -1060,8 +1178,11 @@ static void set_lds_limits() {
     if (done) return;
     done = true;
     const int lim = 160 * 1024;
-    (void)hipFuncSetAttribute((const void *)k_apply_count<BYTE>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_count<BYTE, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_count<BYTE, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              lim);
     (void)hipFuncSetAttribute((const void *)k_apply_bit, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
 #define KH_LDS_MAX(...) (void)hipFuncSetAttribute((const void *)__VA_ARGS__, hipFuncAttributeMaxDynamicSharedMemorySize, lim)
     for (int kpt : {1, 2, 4, 8})
@@ -1075,6 +1196,11 @@ static void set_lds_limits() {
     KH_LDS_MAX((k_scatter_l2<PT_THREADS, 8, L2_RPT>));
     KH_LDS_MAX((k_scatter_l2<PT_THREADS, 16, L2_RPT>));
     KH_LDS_MAX((k_scatter_l2f<PT_THREADS, L2_RPT>));
+    for (int kpt : {1, 2, 4, 8}) {
+        KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt));
+        KH_LDS_MAX(l1f_kernel<SrcBytes>(kpt));
+        KH_LDS_MAX(l1f_kernel<SrcHashes>(kpt));
+    }
     KH_LDS_MAX((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 1>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 2>));
@@ -1155,7 +1281,7 @@ Graph::~Graph() {
     if (stream) (void)hipStreamSynchronize(stream);
     Workspace &w = ws;
     void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.fullf, w.newbits, w.bc, w.bcn, w.bck, w.bcv,
-                    w.off1, w.ch2, w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.xseg, w.reg_base, w.reg_cur, w.ctr, w.d_words, w.d_koff, w.d_bytes,
+                    w.off1, w.ch2, w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.xseg, w.reg_base, w.reg_cur, w.bkt_base, w.bkt_cur, w.ctr, w.d_words, w.d_koff, w.d_bytes,
                     w.q_hashes, w.q_counts, w.frec, w.fcount};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);

@@ -114,6 +114,9 @@ struct Workspace {
     uint64_t *reg_base = nullptr;    // [regions + 1] capacity prefix for passes of reg_nkmers k-mers
     uint64_t *reg_cur = nullptr;     // [regions] append cursors
     uint64_t cap_reg = 0, reg_nkmers = 0, reg_total = 0;
+    // fixed-capacity level 1 (k_scatter_l1f): bucket b holds [bkt_base[b], bkt_cur[b])
+    uint64_t *bkt_base = nullptr, *bkt_cur = nullptr;
+    uint64_t bkt_nkmers = 0, bkt_total = 0;
     uint64_t *ctr = nullptr;         // counters, see CTR_*
     uint64_t *h_ctr = nullptr;       // pinned host mirror
     uint64_t cap_regions = 0, cap_xseg = 0;

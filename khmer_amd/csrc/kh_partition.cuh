@@ -425,6 +425,184 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
 }
 
 // ---------------------------------------------------------------------------
+// Level 1 into fixed-capacity buckets: the k-mers are hashed once (no
+// histogram pass).  Bucket b owns [bkt_base[b], bkt_base[b+1]), sized on the
+// host from its expected record count.  A persistent grid: workgroup w takes
+// k-mers [w * kpw, (w+1) * kpw) tile by tile; each tile is counting-sorted by
+// bucket in LDS as in k_scatter_l1, and its runs are appended to blocks of
+// L1F_BLK records that the workgroup reserves with one returning atomic per
+// (bucket, tile) on bkt_cur[b] (a block belongs to one workgroup, so runs
+// keep their 16-B aligned pairs with 2-record LDS tails).  After its last
+// tile a workgroup fills the rest of its partial blocks with the ~0 sentinel;
+// bucket b's records are then [bkt_base[b], bkt_cur[b]).  A bucket that runs
+// out of capacity sets ctr[CTR_ERR] bit 8 and the host redoes the pass with
+// the exact two-pass level 1.
+constexpr uint32_t L1F_BLK = 256;
+
+template <class Src, int KPT>
+__global__ void __launch_bounds__(L1_THREADS) k_scatter_l1f(Params P, Src src, uint64_t nkmers, uint64_t kpw, int t0,
+                                                           int nt, const uint64_t *bkt_base,
+                                                           unsigned long long *bkt_cur, uint64_t *rec,
+                                                           uint64_t *ctr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int RPT = L1_MAX_RPT;
+    constexpr int TILE_RECS = L1_THREADS * RPT;
+    constexpr int TILE_KMERS = L1_THREADS * KPT;
+    constexpr uint32_t BLK = L1F_BLK;
+    constexpr uint64_t DEAD = ~0ull;
+    const uint32_t F1 = P.F1;
+    const uint32_t F1a = (F1 + 3) & ~3u;
+    uint64_t *bcur = (uint64_t *)smem;                  // [F1] partially filled block (DEAD: overflowed)
+    uint64_t *nbase = bcur + F1a;                       // [F1] blocks reserved for this tile
+    uint64_t *dla = nbase + F1a;                        // [F1] output - LDS position, current block
+    uint64_t *dlb = dla + F1a;                          // [F1] output - LDS position, new blocks
+    uint64_t *stage = dlb + F1a;                        // [TILE_RECS]
+    uint64_t *tail = stage + TILE_RECS;                 // [F1] a pending odd record
+    uint32_t *cnt = (uint32_t *)(tail + F1a);           // [F1] records appended by this workgroup
+    uint32_t *hist = cnt + F1a;                         // [F1]
+    uint32_t *lstart = hist + F1a;                      // [F1]
+    uint32_t *qs = lstart + F1a;                        // [F1] first LDS position in the new blocks
+    uint32_t *qlim = qs + F1a;                          // [F1] first LDS position left for the tail
+    uint16_t *sb = (uint16_t *)(qlim + F1a);            // [TILE_RECS]
+    uint32_t *s_wtot = (uint32_t *)(sb + TILE_RECS);    // [16]
+    uint64_t *s_meta = (uint64_t *)(s_wtot + 16);
+    uint64_t *s_koff = s_meta + 2;
+    const int shift = P.s0 + P.s2;
+    const uint64_t omask = (1ull << shift) - 1;
+    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) {
+        bcur[b] = 0;
+        cnt[b] = 0;
+        hist[b] = 0;
+    }
+    const uint64_t c0 = min(nkmers, (uint64_t)blockIdx.x * kpw);
+    const uint64_t c1 = min(nkmers, c0 + kpw);
+    const bool pre = !needs_window(src);
+    typename Src::Pend pend[KPT];
+    if (pre) {
+#pragma unroll
+        for (int a = 0; a < KPT; a++) {
+            const uint64_t j = c0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            if (j < min(c1, c0 + TILE_KMERS)) pend[a] = kmer_fetch(src, j);
+        }
+    }
+    const uint32_t ntiles = uniform_u32((uint32_t)((c1 - c0 + TILE_KMERS - 1) / TILE_KMERS));
+    for (uint32_t ti = 0; ti < ntiles; ti++) {
+        const uint64_t j0 = c0 + (uint64_t)ti * TILE_KMERS;
+        const uint64_t j1 = min(c1, j0 + TILE_KMERS);
+        const bool last = ti + 1 == ntiles;
+        block_sync();
+        TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
+        uint64_t G[RPT];
+        uint32_t rank[RPT];
+        uint32_t jj[RPT];
+        int nr = 0;
+#pragma unroll
+        for (int q = 0; q < RPT; q++) { G[q] = ~0ull; rank[q] = 0; jj[q] = 0; }
+        uint64_t hh[KPT];
+#pragma unroll
+        for (int a = 0; a < KPT; a++) {
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            hh[a] = j < j1 ? (pre ? src.finish(pend[a]) : kmer_hash(src, s_koff, tr, j)) : 0;
+        }
+#pragma unroll
+        for (int a = 0; a < KPT; a++) {
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            const bool ok = j < j1;
+#pragma unroll
+            for (int q = 0; q < RPT; q++) {
+                const int i = q - a * nt;
+                if (ok && i >= 0 && i < nt) {
+                    uint64_t Gq;
+                    if (local_bin(P, t0 + i, hh[a], &Gq)) {
+                        G[q] = Gq;
+                        jj[q] = (uint32_t)j;
+                        rank[q] = atomicAdd(&hist[(uint32_t)(Gq >> shift)], 1u);
+                        nr = q + 1;
+                    }
+                }
+            }
+        }
+        block_sync();
+        block_scan_hist(hist, lstart, F1, s_wtot);
+        block_sync();
+#pragma unroll
+        for (int q = 0; q < RPT; q++) {
+            if (q < nr && G[q] != ~0ull) {
+                const uint32_t b = (uint32_t)(G[q] >> shift);
+                const uint32_t pos = lstart[b] + rank[q];
+                stage[pos] = ((uint64_t)jj[q] << 32) | (G[q] & omask);
+                sb[pos] = (uint16_t)b;
+            }
+        }
+        if (pre) {
+            const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
+#pragma unroll
+            for (int a = 0; a < KPT; a++) {
+                const uint64_t j = n0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+                if (j < n1) pend[a] = kmer_fetch(src, j);
+            }
+        }
+        // per bucket: block reservation (one atomic when the tile needs new
+        // blocks), the pending odd record when its pair completes, and the
+        // placement constants of this tile's run
+        for (uint32_t d = threadIdx.x; d < F1; d += blockDim.x) {
+            const uint32_t h = hist[d];
+            if (!h && !last) continue;
+            const uint32_t L0 = cnt[d];
+            const uint32_t split = (L0 + BLK - 1) & ~(BLK - 1);
+            const uint32_t need = (L0 + h + BLK - 1) / BLK - split / BLK;
+            uint64_t bc = bcur[d], nb = 0;
+            if (bc == DEAD) {
+                nb = DEAD;
+            } else if (need) {
+                nb = atomicAdd(&bkt_cur[d], (unsigned long long)need * BLK);
+                if (nb + (uint64_t)need * BLK > bkt_base[d + 1]) {
+                    atomicOr((unsigned long long *)&ctr[CTR_ERR], 8ull);
+                    nb = DEAD;
+                }
+            }
+            const uint32_t e = L0 + h, fe = last ? e : (e & ~1u);
+            if ((L0 & 1) && fe > L0 - 1 && bc != DEAD) rec[bc + ((L0 - 1) & (BLK - 1))] = tail[d];
+            const uint32_t q0 = lstart[d];
+            const bool dead = bc == DEAD || nb == DEAD;
+            nbase[d] = nb;
+            dla[d] = bc + (L0 & (BLK - 1)) - q0;
+            dlb[d] = nb + L0 - split - q0;
+            qs[d] = q0 + (split - L0);
+            qlim[d] = dead ? 0 : q0 + (fe > L0 ? fe - L0 : 0);
+        }
+        block_sync();
+        const uint32_t ntile = lstart[F1 - 1] + hist[F1 - 1];
+#pragma unroll
+        for (int u = 0; u < RPT; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * L1_THREADS;
+            if (q >= ntile) continue;
+            const uint32_t d = sb[q];
+            if (q < qlim[d]) rec[(q < qs[d] ? dla[d] : dlb[d]) + q] = stage[q];
+            else tail[d] = stage[q];   // the odd last record of the run (not on the last tile)
+        }
+        block_sync();
+        for (uint32_t d = threadIdx.x; d < F1; d += blockDim.x) {
+            const uint32_t h = hist[d];
+            if (!h) continue;
+            const uint32_t L0 = cnt[d];
+            const uint32_t need = (L0 + h + BLK - 1) / BLK - (L0 + BLK - 1) / BLK;
+            if (nbase[d] == DEAD) bcur[d] = DEAD;
+            else if (need) bcur[d] = nbase[d] + (uint64_t)(need - 1) * BLK;
+            cnt[d] = L0 + h;
+            hist[d] = 0;
+        }
+    }
+    block_sync();
+    for (uint32_t y = threadIdx.x; y < F1 * BLK; y += blockDim.x) {
+        const uint32_t d = y / BLK, sl = y % BLK;
+        const uint32_t c = cnt[d] & (BLK - 1);
+        if (c == 0 || sl < c || bcur[d] == DEAD) continue;
+        rec[bcur[d] + sl] = ~0ull;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Level 1 of a shard ("owned filter").  A shard of a G-rank group owns ~1/G
 // of every table's bins but hashes every k-mer of the stream, so with
 // k_hist_l1 + k_scatter_l1 it would hash each k-mer twice and run the whole
@@ -698,7 +876,8 @@ constexpr uint64_t L2F_DEAD = ~0ull;
 
 template <int THREADS, int RPT>
 __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, int s2, uint32_t parts,
-                                                         const uint64_t *off1, const uint64_t *reg_base,
+                                                         const uint64_t *bstart, const uint64_t *bend,
+                                                         const uint64_t *reg_base,
                                                          unsigned long long *reg_cur, const uint64_t *rec_in,
                                                          uint64_t *rec_out, uint64_t *ctr) {
     constexpr int TILE = THREADS * RPT;
@@ -711,7 +890,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
     uint32_t *cnt = (uint32_t *)(tail + F2 * SEG);  // [F2] records appended by this workgroup
     uint32_t *hist = cnt + F2;                      // [F2] this tile's records
     const uint32_t b = blockIdx.x / parts, p = blockIdx.x % parts;
-    const uint64_t b0 = off1[b], b1 = off1[b + 1];
+    const uint64_t b0 = bstart[b], b1 = bend[b];
     const uint64_t len = (b1 - b0 + parts - 1) / parts;
     const uint64_t r0 = min(b1, b0 + (uint64_t)p * len), r1 = min(b1, r0 + len);
     const uint64_t gb = (uint64_t)b << s2;
