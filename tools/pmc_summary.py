@@ -75,10 +75,12 @@ def timer_name(device_kernel):
     if base.startswith("k_"):
         base = base[2:]
     if base == "apply_count":
-        return {"1": "apply_byte", "7": "apply_nibble"}.get(device_kernel.split("<")[1].split(">")[0], base)
+        kind = device_kernel.split("<")[1].split(">")[0].split(",")[0].strip()
+        return {"1": "apply_byte", "7": "apply_nibble"}.get(kind, base)
     if base == "apply_bit":
         return "apply_bit"
-    return base
+    # the fixed-capacity partitions time under the same names as the exact ones
+    return {"scatter_l1f": "scatter_l1", "scatter_l2f": "scatter_l2"}.get(base, base)
 
 
 if __name__ == "__main__":
