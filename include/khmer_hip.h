@@ -164,7 +164,15 @@ int kh_graph_save(kh_graph *g, const char *path);               /* storage.cc:99
  * expected_storage checks the file type code like the reference readers. */
 int kh_graph_load(const char *path, int expected_storage, int hash_kind, int device,
                   kh_graph **out);
-int kh_graph_n_tags(kh_graph *g, uint64_t *out);
+
+/* header fields of a saved table file, read as raw bytes like the reference's
+ * Python readers (khmer/__init__.py:95-178 extract_nodegraph_info /
+ * extract_countgraph_info).  layout 0: no bigcount byte (nodegraph reader);
+ * layout 1: a bigcount byte unless the type is SMALLCOUNT (countgraph reader).
+ * out[7] = {version, type, use_bigcount (-1 when absent), k, n_tables,
+ * n_occupied, first table size}.  KH_EFILE when the file is short or does not
+ * start with "OXLI". */
+int kh_file_header(const char *path, int layout, int64_t *out);int kh_graph_n_tags(kh_graph *g, uint64_t *out);
 int kh_graph_get_tags(kh_graph *g, uint64_t *out);              /* ascending */
 int kh_graph_add_tag(kh_graph *g, uint64_t h);
 int kh_graph_save_tagset(kh_graph *g, const char *path);        /* hashgraph.cc:55-88 */

@@ -8,7 +8,6 @@ updated by hand-written HIP kernels in libkhmer_hip.so.
 """
 import ctypes
 from collections import namedtuple
-from struct import pack, unpack
 import sys
 
 from . import _lib
@@ -94,76 +93,54 @@ def reverse_complement(sequence):
     return buf.raw[:len(b)].decode("latin-1")
 
 
-def extract_nodegraph_info(filename):
-    """(ksize, table size, n tables, version, type, occupied) of a nodegraph
-    file (khmer/__init__.py:95-136)."""
-    uint_size = len(pack('I', 0))
-    uchar_size = len(pack('B', 0))
-    ulonglong_size = len(pack('Q', 0))
+def _file_header(filename, layout, what):
+    """Header fields through the library's raw reader (kh_file_header); any
+    failure is the reference's "corrupt" ValueError (khmer/__init__.py:95-178)."""
+    out = (ctypes.c_int64 * 7)()
     try:
-        with open(filename, 'rb') as nodegraph:
-            signature, = unpack('4s', nodegraph.read(4))
-            version, = unpack('B', nodegraph.read(1))
-            ht_type, = unpack('B', nodegraph.read(1))
-            ksize, = unpack('I', nodegraph.read(uint_size))
-            n_tables, = unpack('B', nodegraph.read(uchar_size))
-            occupied, = unpack('Q', nodegraph.read(ulonglong_size))
-            table_size, = unpack('Q', nodegraph.read(ulonglong_size))
-        if signature != b"OXLI":
-            raise ValueError("Node graph '{}' is missing file type "
-                             "signature".format(filename) + str(signature))
-    except:  # noqa: E722  (reference behaviour: any failure -> corrupt)
-        raise ValueError("Node graph '{}' is corrupt ".format(filename))
-    return ksize, round(table_size, -2), n_tables, version, ht_type, occupied
+        check(lib.kh_file_header(str(filename).encode(), layout, out))
+    except (OSError, ValueError, TypeError):
+        raise ValueError("{} '{}' is corrupt ".format(what, filename))
+    version, ht_type, bigcount, ksize, n_tables, occupied, size0 = list(out)
+    return version, ht_type, (None if bigcount < 0 else bigcount), ksize, n_tables, occupied, size0
+
+
+def extract_nodegraph_info(filename):
+    """(ksize, table size rounded to 100, n tables, version, type, occupied)
+    of a saved nodegraph."""
+    version, ht_type, _, ksize, n_tables, occupied, size0 = _file_header(filename, 0, "Node graph")
+    return ksize, round(size0, -2), n_tables, version, ht_type, occupied
+
+
+CgInfo = namedtuple("CgInfo", ["ksize", "n_tables", "table_size", "use_bigcount", "version", "ht_type",
+                               "n_occupied"])
 
 
 def extract_countgraph_info(filename):
-    """CgInfo of a countgraph file (khmer/__init__.py:139-178)."""
-    CgInfo = namedtuple("CgInfo", ['ksize', 'n_tables', 'table_size', 'use_bigcount',
-                                   'version', 'ht_type', 'n_occupied'])
-    uint_size = len(pack('I', 0))
-    ulonglong_size = len(pack('Q', 0))
-    try:
-        with open(filename, 'rb') as countgraph:
-            signature, = unpack('4s', countgraph.read(4))
-            version, = unpack('B', countgraph.read(1))
-            ht_type, = unpack('B', countgraph.read(1))
-            if ht_type != FILETYPES['SMALLCOUNT']:
-                use_bigcount, = unpack('B', countgraph.read(1))
-            else:
-                use_bigcount = None
-            ksize, = unpack('I', countgraph.read(uint_size))
-            n_tables, = unpack('B', countgraph.read(1))
-            occupied, = unpack('Q', countgraph.read(ulonglong_size))
-            table_size, = unpack('Q', countgraph.read(ulonglong_size))
-        if signature != b'OXLI':
-            raise ValueError("Count graph file '{}' is missing file type "
-                             "signature. ".format(filename) + str(signature))
-    except:  # noqa: E722
-        raise ValueError("Count graph file '{}' is corrupt ".format(filename))
-    return CgInfo(ksize, n_tables, round(table_size, -2), use_bigcount, version, ht_type, occupied)
+    """CgInfo of a saved countgraph (use_bigcount is None for SMALLCOUNT files)."""
+    version, ht_type, bigcount, ksize, n_tables, occupied, size0 = _file_header(filename, 1, "Count graph file")
+    return CgInfo(ksize, n_tables, round(size0, -2), bigcount, version, ht_type, occupied)
+
+
+_TOO_SMALL = """**
+** ERROR: the graph structure is too small for 
+** this data set.  Increase data structure size
+** with --max_memory_usage/-M.
+**
+** Do not use these results!!
+**
+** (estimated false positive rate of {fp:.3f}; max recommended {mx:.3f})
+**"""
 
 
 def calc_expected_collisions(graph, force=False, max_false_pos=.2):
-    """Expected false-positive rate from table-0 occupancy
-    (khmer/__init__.py:181-215)."""
+    """False-positive rate expected from table-0 occupancy: (occupied / the
+    smallest table) ** n_tables.  Above max_false_pos it prints the
+    reference's warning block and exits 1 unless force."""
     sizes = graph.hashsizes()
-    n_ht = float(len(sizes))
-    occupancy = float(graph.n_occupied())
-    min_size = min(sizes)
-    fp_one = occupancy / min_size
-    fp_all = fp_one ** n_ht
+    fp_all = (float(graph.n_occupied()) / min(sizes)) ** float(len(sizes))
     if fp_all > max_false_pos:
-        print("**", file=sys.stderr)
-        print("** ERROR: the graph structure is too small for ", file=sys.stderr)
-        print("** this data set.  Increase data structure size", file=sys.stderr)
-        print("** with --max_memory_usage/-M.", file=sys.stderr)
-        print("**", file=sys.stderr)
-        print("** Do not use these results!!", file=sys.stderr)
-        print("**", file=sys.stderr)
-        print("** (estimated false positive rate of %.3f;" % fp_all, file=sys.stderr, end=' ')
-        print("max recommended %.3f)" % max_false_pos, file=sys.stderr)
-        print("**", file=sys.stderr)
+        print(_TOO_SMALL.format(fp=fp_all, mx=max_false_pos), file=sys.stderr)
         if not force:
             sys.exit(1)
     return fp_all

@@ -79,6 +79,7 @@ SIGNATURES = {
     "kh_graph_copy_table": (i32, [P, i32, ctypes.c_void_p]),
     "kh_graph_save": (i32, [P, ctypes.c_char_p]),
     "kh_graph_load": (i32, [ctypes.c_char_p, i32, i32, i32, ctypes.POINTER(P)]),
+    "kh_file_header": (i32, [ctypes.c_char_p, i32, ctypes.POINTER(ctypes.c_int64)]),
     "kh_graph_n_tags": (i32, [P, PU64]),
     "kh_graph_get_tags": (i32, [P, PU64]),
     "kh_graph_add_tag": (i32, [P, u64]),

@@ -772,6 +772,61 @@ __global__ void k_bc_compact(const uint64_t *bck, const uint32_t *bcv, uint64_t 
 }
 
 // ---------------------------------------------------------------------------
+// Small passes (a single add(), one short consume()): the reference's
+// per-k-mer Storage::add (storage.hh:172-199, 320-359, 571-624) in stream
+// order by one wavefront, lane i owning table i, instead of the partition
+// pipeline whose fixed cost grows with the table size.  flags[j]: bit 0
+// is_new, bit 1 table-0 first touch (n_occupied), bit 2 full in every table
+// (a bigcount event); hashes[j] the k-mer's hash.  Not for shards.
+template <class Src>
+__global__ void __launch_bounds__(64) k_small_pass(Params P, Src src, uint64_t nkmers, uint8_t *tab, uint8_t *flags,
+                                                   uint64_t *hashes) {
+    __shared__ uint64_t sh[64];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t nmask = P.n >= 64 ? ~0ull : ((1ull << P.n) - 1);
+    for (uint64_t j0 = 0; j0 < nkmers; j0 += 64) {
+        const uint64_t j = j0 + lane;
+        if (j < nkmers) {
+            const uint64_t h = kmer_hash_global(src, j);
+            sh[lane] = h;
+            hashes[j] = h;
+        }
+        block_sync();
+        const uint32_t m = (uint32_t)min<uint64_t>(64, nkmers - j0);
+        for (uint32_t u = 0; u < m; u++) {
+            const uint64_t h = sh[u];
+            bool zero = false, full = false;
+            if ((int)lane < P.n) {
+                const uint64_t bin = mod_barrett(h, P.p[lane], P.m[lane]);
+                uint8_t *t = tab + P.tbyte[lane];
+                if (P.kind == BIT) {
+                    const uint8_t bit = (uint8_t)(1u << (bin & 7));
+                    const uint8_t v = t[bin >> 3];
+                    zero = !(v & bit);
+                    t[bin >> 3] = v | bit;
+                } else if (P.kind == NIBBLE) {   // even bin -> high nibble (storage.hh:262-272)
+                    const int sh4 = (bin & 1) ? 0 : 4;
+                    const uint8_t v = t[bin >> 1];
+                    const uint32_t cur = (v >> sh4) & 15u;
+                    zero = cur == 0;
+                    if (cur < 15) t[bin >> 1] = (uint8_t)((v & ~(15u << sh4)) | ((cur + 1) << sh4));
+                } else {
+                    const uint32_t cur = t[bin];
+                    zero = cur == 0;
+                    if (cur < 255) t[bin] = (uint8_t)(cur + 1);
+                    else full = true;
+                }
+            }
+            const uint64_t zb = __ballot(zero) & nmask, fb = __ballot(full) & nmask;
+            if (lane == 0)
+                flags[j0 + u] = (uint8_t)((zb ? 1 : 0) | ((zb & 1) ? 2 : 0) |
+                                          (P.kind == BYTE && P.use_bigcount && fb == nmask ? 4 : 0));
+        }
+        block_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // sharded groups (kh_engine.hip group_*): winners of every shard are routed to
 // the rank owning their k-mer window; full events are merged on every rank
 

@@ -639,6 +639,36 @@ struct In {
     ~In() { if (gz) gzclose(gz); }
 };
 
+// raw header reader for khmer.extract_*_info (see include/khmer_hip.h)
+extern "C" int kh_file_header(const char *path, int layout, int64_t *out) {
+    return guard([&] {
+        CHECK_PTR(path);
+        CHECK_PTR(out);
+        FILE *f = fopen(path, "rb");
+        if (!f) fail(KH_EFILE, std::string("cannot open ") + path);
+        unsigned char buf[32];
+        const size_t got = fread(buf, 1, sizeof buf, f);
+        fclose(f);
+        size_t at = 0;
+        auto take = [&](size_t n) -> uint64_t {
+            if (at + n > got) fail(KH_EFILE, std::string("short header in ") + path);
+            uint64_t v = 0;
+            for (size_t b = 0; b < n; b++) v |= (uint64_t)buf[at + b] << (8 * b);
+            at += n;
+            return v;
+        };
+        take(4);
+        if (memcmp(buf, "OXLI", 4) != 0) fail(KH_EFILE, std::string("missing OXLI signature in ") + path);
+        out[0] = (int64_t)take(1);
+        out[1] = (int64_t)take(1);
+        out[2] = (layout == 1 && out[1] != NIBBLE) ? (int64_t)take(1) : -1;
+        out[3] = (int64_t)take(4);
+        out[4] = (int64_t)take(1);
+        out[5] = (int64_t)take(8);
+        out[6] = (int64_t)take(8);
+    });
+}
+
 extern "C" int kh_graph_load(const char *path, int expected_storage, int hash_kind, int device, kh_graph **out) {
     return guard([&] {
         In in;

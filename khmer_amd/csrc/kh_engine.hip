@@ -822,9 +822,45 @@ static void pass_stage_c(Graph *g, const Src &src, PassState &ps, const PassOut 
     if (bigc) bcmap_merge(g, w.h_ctr[CTR_NBC], w.h_ctr[CTR_BCFF]);
 }
 
+// passes of at most SMALL_PASS k-mers run k_small_pass (sequential semantics,
+// no partition); KH_SMALL_PASS overrides the threshold (0 disables)
+static uint64_t small_pass_max() { return (uint64_t)std::max(0, env_seg("KH_SMALL_PASS", 2048)); }
+
+template <class Src>
+static void run_pass_small(Graph *g, const Src &src, uint64_t nkmers, const PassOut *out) {
+    Workspace &w = g->ws;
+    hipStream_t st = g->stream;
+    ensure((void **)&w.sm_flags, &w.cap_sm, nkmers, 1);
+    ensure((void **)&w.sm_hash, &w.cap_smh, nkmers, 8);
+    TIMED("small_pass", hipLaunchKernelGGL(k_small_pass<Src>, dim3(1), dim3(64), 0, st, g->prm, src, nkmers, g->d_tab,
+                                           w.sm_flags, w.sm_hash));
+    KH_HIP(hipGetLastError());
+    std::vector<uint8_t> fl(nkmers);
+    std::vector<uint64_t> hs(nkmers);
+    KH_HIP(hipMemcpyAsync(fl.data(), w.sm_flags, nkmers, hipMemcpyDeviceToHost, st));
+    KH_HIP(hipMemcpyAsync(hs.data(), w.sm_hash, nkmers * 8, hipMemcpyDeviceToHost, st));
+    KH_HIP(hipStreamSynchronize(st));
+    engine_collect_events(g);
+    for (uint64_t j = 0; j < nkmers; j++) {
+        g->n_unique += fl[j] & 1;
+        g->n_occupied += (fl[j] >> 1) & 1;
+        if (fl[j] & 4) {   // ByteStorage::add bigcount update (storage.hh:606-616)
+            auto it = g->bigcounts.find(hs[j]);
+            g->bigcounts[hs[j]] = it == g->bigcounts.end() ? 256 : (uint16_t)std::min<uint32_t>(it->second + 1u, 65535u);
+            g->bc_dirty = true;
+        }
+        if (out && out->h_new) out->h_new[j] = fl[j] & 1;
+        if (out && out->h_hash) out->h_hash[j] = hs[j];
+    }
+}
+
 template <class Src>
 static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *out) {
     if (nkmers == 0) return;
+    if (nkmers <= small_pass_max() && g->world == 1) {
+        run_pass_small(g, src, nkmers, out);
+        return;
+    }
     PassState ps = pass_stage_a(g, src, nkmers);
     pass_mark_local(g, ps, out && out->h_new);
     pass_stage_c(g, src, ps, out);

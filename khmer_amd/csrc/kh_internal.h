@@ -124,6 +124,10 @@ struct Workspace {
     uint64_t *d_words = nullptr, *d_koff = nullptr;
     uint8_t *d_bytes = nullptr;
     uint64_t cap_words = 0, cap_koff = 0, cap_bytes = 0;
+    // small passes (k_small_pass): per-k-mer flags and hashes
+    uint8_t *sm_flags = nullptr;
+    uint64_t *sm_hash = nullptr;
+    uint64_t cap_sm = 0, cap_smh = 0;
     // query staging
     uint64_t *q_hashes = nullptr;
     uint16_t *q_counts = nullptr;

@@ -87,11 +87,22 @@ class Hashtable(object):
             check(lib.kh_hash_twobit(b, self._k, None, None, ctypes.byref(out)))
         return out.value
 
-    def _refresh_mirrors(self):
-        if self._mirrors:
-            for i, buf in enumerate(self._mirrors):
-                ptr = (ctypes.c_char * len(buf)).from_buffer(buf)
-                check(lib.kh_graph_copy_table(self._g, i, ptr))
+    # Host mirrors behind get_raw_tables(): up to this many bytes they are
+    # re-copied after every mutating call, so views handed out earlier track
+    # the device tables like the reference's aliasing views
+    # (graphs.pyx:333-347); larger tables are re-copied only when
+    # get_raw_tables() is called again (a GB-sized copy per add() would cost
+    # seconds).
+    _MIRROR_EAGER_BYTES = 256 << 20
+
+    def _refresh_mirrors(self, force=False):
+        if not self._mirrors:
+            return
+        if not force and sum(len(b) for b in self._mirrors) > self._MIRROR_EAGER_BYTES:
+            return
+        for i, buf in enumerate(self._mirrors):
+            ptr = (ctypes.c_char * len(buf)).from_buffer(buf)
+            check(lib.kh_graph_copy_table(self._g, i, ptr))
 
     # ---- single k-mer operations (graphs.pyx:85-132) ----
     def count(self, kmer):
@@ -371,7 +382,7 @@ class Hashtable(object):
         the device tables like the reference's aliasing views."""
         if self._mirrors is None:
             self._mirrors = [bytearray(n) for n in self._raw_sizes()]
-        self._refresh_mirrors()
+        self._refresh_mirrors(force=True)
         return [memoryview(b).toreadonly() for b in self._mirrors]
 
 

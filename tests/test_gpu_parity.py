@@ -390,3 +390,30 @@ def test_bigcount_map_growth(batch):
     want = o.bigcounts()
     assert len(want) > (1 << 20)
     assert dict(zip(keys, vals)) == want
+
+
+@pytest.mark.parametrize("small", ["0", "2048", "100000"])
+@pytest.mark.parametrize("cls", ["Countgraph", "SmallCountgraph", "Nodegraph"])
+def test_small_pass_threshold(monkeypatch, cls, small):
+    """The sequential small-pass kernel and the partition pipeline give the
+    same exact results (KH_SMALL_PASS: passes up to that many k-mers go
+    sequential; 0 disables it)."""
+    monkeypatch.setenv("KH_SMALL_PASS", small)
+    sizes = O.get_n_primes_near_x(4, 1e4)
+    g, o = make_pair(cls, 12, sizes, bigcount=(cls == "Countgraph"))
+    for fname in ("test-abund-read-2.fa", "random-20-a.fa"):
+        assert g.consume_seqfile(data(fname)) == o.consume_fastx(data(fname))
+    for s in ("A" * 400, "ACGT" * 120):
+        assert g.consume(s) == o.consume(s)
+    for h in (5, 5, 17, 99991):
+        assert g.add(h) == bool(o.add(h))
+    assert_same(g, o, "small pass %s" % small)
+    if cls == "Countgraph":
+        import ctypes
+        from khmer_amd._lib import lib, check
+        n = ctypes.c_uint64()
+        check(lib.kh_graph_get_bigcounts(g._g, None, None, 0, ctypes.byref(n)))
+        keys = (ctypes.c_uint64 * max(n.value, 1))()
+        vals = (ctypes.c_uint16 * max(n.value, 1))()
+        check(lib.kh_graph_get_bigcounts(g._g, keys, vals, n.value, ctypes.byref(n)))
+        assert dict(zip(keys[:n.value], vals[:n.value])) == o.bigcounts()
