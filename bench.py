@@ -89,29 +89,88 @@ def kernel_stats(lib, g):
     return out
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_threads():
+    """CPU threads this process may use: the affinity set, capped by
+    OMP_NUM_THREADS (the GPU box's per-job CPU share; nproc there shows the
+    whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(args, sizes):
-    """The oracle (C restatement, 1 thread) on a bounded sample of the same
-    synthetic stream into the same-size tables."""
+    """The oracle (C restatement of Hashtable::consume_string / consume_seqfile,
+    oracle/khmer_oracle.c) on bounded samples of the same synthetic stream into
+    same-size tables, on this host's cores:
+      * in-memory batch, T = host_threads() (the reference's -T N mode: atomic
+        byte updates, src/oxli/hashtable.cc:125-150)  -> `value`
+      * in-memory batch, T = 1 (stream order, the exact semantics)
+      * end to end from a page-cached FASTQ file, T = 1 (parse + clean + count)
+    """
     from oracle import oracle as O
     from khmer_amd import synth
-    t = O.Table(getattr(O, ORACLE_KIND[args.graph]), args.k, sizes)
-    t.set_use_bigcount(args.bigcount)
-    total, secs = 0, 0.0
+    kind = getattr(O, ORACLE_KIND[args.graph])
+    n = args.cpu_reads
     chunk = 100_000
-    for r0 in range(0, args.cpu_reads, chunk):
-        seqs, offs = synth.batch(r0, min(chunk, args.cpu_reads - r0), args.read_len)
-        offs = [int(v) for v in offs]
+    batches = []
+    for r0 in range(0, n, chunk):
+        seqs, offs = synth.batch(r0, min(chunk, n - r0), args.read_len)
+        batches.append((seqs, [int(v) for v in offs]))
+
+    def run(threads):
+        t = O.Table(kind, args.k, sizes)
+        t.set_use_bigcount(args.bigcount)
+        total, secs = 0, 0.0
+        for seqs, offs in batches:
+            t0 = time.perf_counter()
+            total += t.consume_batch(seqs, offs, threads=threads if threads > 1 else 0)
+            secs += time.perf_counter() - t0
+        return total, secs
+
+    T = host_threads()
+    k1, s1 = run(1)
+    kT, sT = run(T)
+    # end to end: FASTQ in the page cache (written, then read once untimed)
+    import tempfile
+    nfq = min(n, 500_000)
+    e2e = None
+    with tempfile.TemporaryDirectory() as tmp:
+        fq = os.path.join(tmp, "sample.fq")
+        synth.write_fastq(fq, nfq, args.read_len)
+        with open(fq, "rb") as fh:
+            while fh.read(1 << 24):
+                pass
+        t = O.Table(kind, args.k, sizes)
+        t.set_use_bigcount(args.bigcount)
         t0 = time.perf_counter()
-        total += t.consume_batch(seqs, offs)
-        secs += time.perf_counter() - t0
+        _, kmers = t.consume_fastx(fq)
+        e2e = kmers / (time.perf_counter() - t0)
     return {
-        "value": total / secs,
+        "value": kT / sT,
         "unit": "k-mers/s",
-        "cores": 1,
+        "cores": T,
         "kind": "port",
-        "sample": "%d synthetic %d bp reads (%d k-mers, the first reads of the benchmark stream) "
-                  "into the same %dx%.0e %s, oracle/khmer_oracle.c single thread"
-                  % (args.cpu_reads, args.read_len, total, args.tables, args.x, args.graph),
+        "cpu_model": cpu_model(),
+        "t1_in_memory": k1 / s1,
+        "tN_in_memory": kT / sT,
+        "t1_end_to_end_fastq": e2e,
+        "sample": "%d synthetic %d bp reads (%d k-mers, the first reads of the benchmark stream) into the same "
+                  "%dx%.0e %s; oracle/khmer_oracle.c: value = %d threads with the reference's -T N atomic "
+                  "updates, t1 = single-threaded stream order, end-to-end = %d reads parsed from a "
+                  "page-cached FASTQ, 1 thread" % (n, args.read_len, k1, args.tables, args.x, args.graph, T, nfq),
     }
 
 

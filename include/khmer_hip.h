@@ -213,6 +213,28 @@ int kh_group_unique_id(unsigned char *out, size_t cap);   /* cap >= 128 */
 int kh_group_create(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables, int world, int rank,
                     int nlocal, const int *devices, const unsigned char *uid, kh_group **out);
 void kh_group_destroy(kh_group *grp);
+/* A one-shard-per-process group whose collectives run through host callbacks
+ * instead of RCCL (a "host transport"): every call is collective over the
+ * group, buffers are host memory, a nonzero return is an error.  Used to run
+ * the multi-process protocol where RCCL cannot (several ranks on one device,
+ * CPU-side plumbing such as gloo or a TCP rendezvous).
+ *   allgather: recv[world * bytes] = every rank's `bytes` bytes, in rank order
+ *   broadcast: buf (bytes) of rank `root` to every rank
+ *   alltoallv: rank r's send holds the blocks for ranks 0..world-1 back to
+ *              back (send_bytes[d] each); recv gets the blocks from ranks
+ *              0..world-1 back to back (recv_bytes[s] each) */
+typedef struct kh_transport {
+    void *ctx;
+    int (*allgather)(void *ctx, const void *send, void *recv, uint64_t bytes);
+    int (*broadcast)(void *ctx, void *buf, uint64_t bytes, int root);
+    int (*alltoallv)(void *ctx, const void *send, const uint64_t *send_bytes, void *recv,
+                     const uint64_t *recv_bytes);
+} kh_transport;
+int kh_group_create_hosted(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables, int world,
+                           int rank, int device, const kh_transport *transport, kh_group **out);
+/* RCCL view of a one-shard-per-process group: ncclCommCount / ncclCommCuDevice
+ * (nranks = 0 and device = -1 for loopback and host-transport groups) */
+int kh_group_comm_info(kh_group *grp, int *nranks, int *device);
 /* local shard l as a graph handle (view: valid while the group lives; its
  * tables are the slices [lo, lo + size) reported by kh_group_slice) */
 int kh_group_shard(kh_group *grp, int l, kh_graph **out);

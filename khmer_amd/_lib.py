@@ -58,6 +58,8 @@ SIGNATURES = {
     "kh_graph_get_bigcounts": (i32, [P, PU64, ctypes.POINTER(ctypes.c_uint16), u64, PU64]),
     "kh_group_unique_id": (i32, [ctypes.c_char_p, sz]),
     "kh_group_create": (i32, [i32, i32, i32, PU64, i32, i32, i32, i32, PI, ctypes.c_char_p, ctypes.POINTER(P)]),
+    "kh_group_create_hosted": (i32, [i32, i32, i32, PU64, i32, i32, i32, i32, P, ctypes.POINTER(P)]),
+    "kh_group_comm_info": (i32, [P, PI, PI]),
     "kh_group_destroy": (None, [P]),
     "kh_group_shard": (i32, [P, i32, ctypes.POINTER(P)]),
     "kh_group_info": (i32, [P, PI, PI, PI]),

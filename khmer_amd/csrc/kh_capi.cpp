@@ -953,6 +953,28 @@ extern "C" int kh_group_create(int storage, int hash_kind, int k, const uint64_t
     });
 }
 
+extern "C" int kh_group_create_hosted(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables,
+                                      int world, int rank, int device, const kh_transport *transport,
+                                      kh_group **out) {
+    return guard([&] {
+        CHECK_PTR(sizes);
+        CHECK_PTR(transport);
+        CHECK_PTR(out);
+        *out = nullptr;
+        ShardGroup *G = group_create_hosted(storage, hash_kind, k, sizes, n_tables, world, rank, device, transport);
+        *out = new kh_group{G};
+    });
+}
+
+extern "C" int kh_group_comm_info(kh_group *grp, int *nranks, int *device) {
+    return guard([&] {
+        CHECK_PTR(grp);
+        CHECK_PTR(nranks);
+        CHECK_PTR(device);
+        group_comm_info(grp->G, nranks, device);
+    });
+}
+
 extern "C" void kh_group_destroy(kh_group *grp) {
     if (!grp) return;
     group_destroy(grp->G);

@@ -1363,6 +1363,8 @@ struct ShardGroup {
     std::vector<Graph *> shards;
     ncclComm_t comm = nullptr;
     ncclComm_t comm_b = nullptr;     // source-read broadcasts (own stream, overlapped with compute)
+    bool hosted = false;             // one shard per process, collectives through host callbacks
+    kh_transport tp{};
     struct Local {
         uint64_t *src = nullptr;
         uint64_t cap_src = 0;        // broadcast reads of another rank (RCCL)
@@ -1413,6 +1415,51 @@ struct ShardGroup {
 
 constexpr uint64_t FULL_LIST_CAP = 1ull << 24;
 
+// ---- collectives of a one-shard-per-process group: RCCL, or the host
+// transport (staged through host memory, synchronous with the stream) ----
+static bool per_rank(const ShardGroup *G) { return G->comm != nullptr || G->hosted; }
+
+static void host_rc(int rc, const char *what) {
+    if (rc) fail(KH_EDEVICE, std::string("host transport: ") + what + " failed");
+}
+
+static void coll_allgather_u64(ShardGroup *G, hipStream_t st, const uint64_t *d_send, uint64_t *d_recv, uint64_t n) {
+    if (G->comm) {
+        KH_NCCL(ncclAllGather(d_send, d_recv, n, ncclUint64, G->comm, st));
+        return;
+    }
+    std::vector<uint64_t> snd(n), rcv(n * (uint64_t)G->world);
+    KH_HIP(hipMemcpyAsync(snd.data(), d_send, n * 8, hipMemcpyDeviceToHost, st));
+    KH_HIP(hipStreamSynchronize(st));
+    host_rc(G->tp.allgather(G->tp.ctx, snd.data(), rcv.data(), n * 8), "allgather");
+    KH_HIP(hipMemcpyAsync(d_recv, rcv.data(), rcv.size() * 8, hipMemcpyHostToDevice, st));
+    KH_HIP(hipStreamSynchronize(st));
+}
+
+enum { RED_SUM, RED_MAX, RED_MIN };
+static void coll_allreduce_u64(ShardGroup *G, hipStream_t st, const uint64_t *d_send, uint64_t *d_recv, uint64_t n,
+                               int op) {
+    if (G->comm) {
+        const ncclRedOp_t o = op == RED_SUM ? ncclSum : op == RED_MAX ? ncclMax : ncclMin;
+        KH_NCCL(ncclAllReduce(d_send, d_recv, n, ncclUint64, o, G->comm, st));
+        return;
+    }
+    std::vector<uint64_t> snd(n), rcv(n * (uint64_t)G->world), red(n);
+    KH_HIP(hipMemcpyAsync(snd.data(), d_send, n * 8, hipMemcpyDeviceToHost, st));
+    KH_HIP(hipStreamSynchronize(st));
+    host_rc(G->tp.allgather(G->tp.ctx, snd.data(), rcv.data(), n * 8), "allreduce");
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t v = rcv[i];
+        for (int r = 1; r < G->world; r++) {
+            const uint64_t x = rcv[(uint64_t)r * n + i];
+            v = op == RED_SUM ? v + x : op == RED_MAX ? std::max(v, x) : std::min(v, x);
+        }
+        red[i] = v;
+    }
+    KH_HIP(hipMemcpyAsync(d_recv, red.data(), n * 8, hipMemcpyHostToDevice, st));
+    KH_HIP(hipStreamSynchronize(st));
+}
+
 void group_unique_id(unsigned char *out, size_t n) {
     ncclUniqueId id;
     if (n < sizeof id) fail(KH_EVALUE, "unique id buffer too small");
@@ -1444,6 +1491,32 @@ ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n
     return G.release();
 }
 
+ShardGroup *group_create_hosted(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank,
+                                int device, const kh_transport *t) {
+    if (world < 1 || world > 64) fail(KH_EVALUE, "group size must be in [1, 64]");
+    if (rank < 0 || rank >= world) fail(KH_EVALUE, "invalid rank");
+    if (!t->allgather || !t->broadcast || !t->alltoallv) fail(KH_EVALUE, "incomplete host transport");
+    std::unique_ptr<ShardGroup> G(new ShardGroup());
+    G->world = world;
+    G->nlocal = 1;
+    G->rank0 = rank;
+    G->hosted = true;
+    G->tp = *t;
+    G->shards.push_back(graph_create_shard(kind, hash, k, sizes, n, device, world, rank));
+    G->loc.resize(1);
+    KH_HIP(hipSetDevice(device));
+    KH_HIP(hipMalloc((void **)&G->d_red, 256 * 8));
+    return G.release();
+}
+
+void group_comm_info(ShardGroup *G, int *nranks, int *device) {
+    *nranks = 0;
+    *device = -1;
+    if (!G->comm) return;
+    KH_NCCL(ncclCommCount(G->comm, nranks));
+    KH_NCCL(ncclCommCuDevice(G->comm, device));
+}
+
 void group_destroy(ShardGroup *G) { delete G; }
 
 static uint32_t group_wlo(uint32_t FJ, int W, int r) { return (uint32_t)((uint64_t)FJ * (uint64_t)r / (uint64_t)W); }
@@ -1464,10 +1537,10 @@ static void group_route_winners(ShardGroup *G, std::vector<PassState> &ps) {
                                           g->ws.moff, g->ws.mcnt, ps[l].q.nchw, FJ, lc.ws));
     }
     G->h_ws.assign((size_t)W * (FJ + 1), 0);
-    if (G->comm) {
+    if (per_rank(G)) {
         Graph *g = G->shards[0];
         auto &lc = G->loc[0];
-        KH_NCCL(ncclAllGather(lc.ws, lc.ws_all, FJ + 1, ncclUint64, G->comm, g->stream));
+        coll_allgather_u64(G, g->stream, lc.ws, lc.ws_all, FJ + 1);
         KH_HIP(hipMemcpyAsync(G->h_ws.data(), lc.ws_all, G->h_ws.size() * 8, hipMemcpyDeviceToHost, g->stream));
         KH_HIP(hipStreamSynchronize(g->stream));
     } else {
@@ -1512,6 +1585,21 @@ static void group_route_winners(ShardGroup *G, std::vector<PassState> &ps) {
                 if (cin) KH_NCCL(ncclRecv(lc.recv + roff[d], cin, ncclUint32, d, G->comm, g->stream));
             }
             KH_NCCL(ncclGroupEnd());
+        } else if (G->hosted) {
+            // the rank's winners are partitioned by window, so the blocks for
+            // ranks 0..W-1 lie back to back: one alltoallv
+            std::vector<uint64_t> sb(W), rb(W);
+            for (int d = 0; d < W; d++) {
+                sb[d] = 4 * (wsv(r, group_wlo(FJ, W, d + 1)) - wsv(r, group_wlo(FJ, W, d)));
+                rb[d] = 4 * (wsv(d, wh) - wsv(d, wl));
+            }
+            const uint64_t nsend = wsv(r, FJ) - wsv(r, 0);
+            std::vector<uint32_t> hs(nsend + 1), hr(tot + 1);
+            KH_HIP(hipMemcpyAsync(hs.data(), ps[0].wout + wsv(r, 0), nsend * 4, hipMemcpyDeviceToHost, g->stream));
+            KH_HIP(hipStreamSynchronize(g->stream));
+            host_rc(G->tp.alltoallv(G->tp.ctx, hs.data(), sb.data(), hr.data(), rb.data()), "alltoallv");
+            KH_HIP(hipMemcpyAsync(lc.recv, hr.data(), tot * 4, hipMemcpyHostToDevice, g->stream));
+            KH_HIP(hipStreamSynchronize(g->stream));
         } else {
             for (int s = 0; s < W; s++) {
                 const uint64_t c = wsv(s, wh) - wsv(s, wl);
@@ -1554,11 +1642,11 @@ static void group_merge_full(ShardGroup *G, std::vector<PassState> &ps) {
         }
         cnt[G->rank0 + l] = h[CTR_NFULL];
     }
-    if (G->comm) {
+    if (per_rank(G)) {
         Graph *g = G->shards[0];
         auto &lc = G->loc[0];
         KH_HIP(hipMemcpyAsync(G->d_red + 128, &cnt[G->rank0], 8, hipMemcpyHostToDevice, g->stream));
-        KH_NCCL(ncclAllGather(G->d_red + 128, G->d_red, 1, ncclUint64, G->comm, g->stream));
+        coll_allgather_u64(G, g->stream, G->d_red + 128, G->d_red, 1);
         KH_HIP(hipMemcpyAsync(cnt.data(), G->d_red, W * 8, hipMemcpyDeviceToHost, g->stream));
         KH_HIP(hipStreamSynchronize(g->stream));
         const uint64_t mx = *std::max_element(cnt.begin(), cnt.end());
@@ -1576,7 +1664,7 @@ static void group_merge_full(ShardGroup *G, std::vector<PassState> &ps) {
         if (mx > cnt[G->rank0])
             KH_HIP(hipMemsetAsync(lc.flist + cnt[G->rank0], 0xFF, (mx - cnt[G->rank0]) * 8, g->stream));
         ensure((void **)&lc.fall, &lc.cap_fall, (uint64_t)W * mx, 8);
-        KH_NCCL(ncclAllGather(lc.flist, lc.fall, mx, ncclUint64, G->comm, g->stream));
+        coll_allgather_u64(G, g->stream, lc.flist, lc.fall, mx);
         KH_HIP(hipMemsetAsync(g->ws.fullf, 0, (nk + 15) & ~15ull, g->stream));
         hipLaunchKernelGGL(k_full_scatter, dim3(2048), dim3(256), 0, g->stream, lc.fall, (uint64_t)W * mx,
                            g->ws.fullf);
@@ -1605,13 +1693,13 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
     const int k = g0->k;
     if (g0->hash != TWOBIT) fail(KH_EVALUE, "sharded consume takes 2-bit packed reads");
     if (read_len < (uint64_t)k) fail(KH_EVALUE, "reads shorter than k");
-    if (G->comm) {
+    if (per_rank(G)) {
         // every rank must pass the same shape (collective schedule depends on it)
         uint64_t h[2] = {nreads, read_len};
         KH_HIP(hipSetDevice(g0->device));
         KH_HIP(hipMemcpyAsync(G->d_red + 140, h, 16, hipMemcpyHostToDevice, g0->stream));
-        KH_NCCL(ncclAllReduce(G->d_red + 140, G->d_red + 142, 2, ncclUint64, ncclMax, G->comm, g0->stream));
-        KH_NCCL(ncclAllReduce(G->d_red + 140, G->d_red + 144, 2, ncclUint64, ncclMin, G->comm, g0->stream));
+        coll_allreduce_u64(G, g0->stream, G->d_red + 140, G->d_red + 142, 2, RED_MAX);
+        coll_allreduce_u64(G, g0->stream, G->d_red + 140, G->d_red + 144, 2, RED_MIN);
         uint64_t mm[4];
         KH_HIP(hipMemcpyAsync(mm, G->d_red + 142, 32, hipMemcpyDeviceToHost, g0->stream));
         KH_HIP(hipStreamSynchronize(g0->stream));
@@ -1640,14 +1728,28 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
         for (int b = 0; b < 2; b++) lc.freed[b] = false;   // each slot's last reader is done (synchronised)
     }
     const bool rccl = G->comm != nullptr;
-    auto own = [&](int s, int l) { return rccl && G->rank0 + l == s; };
+    auto own = [&](int s, int l) { return per_rank(G) && G->rank0 + l == s; };
     auto transfer = [&](int s) {
         for (int l = 0; l < NL; l++) {
             auto &lc = G->loc[l];
             const int b = s & 1;
             KH_HIP(hipSetDevice(G->shards[l]->device));
             if (lc.freed[b]) KH_HIP(hipStreamWaitEvent(lc.st_x, lc.ev_free[b], 0));
-            if (own(s, l)) {
+            if (G->hosted) {
+                // synchronous: the root's reads through host memory into the slot
+                std::vector<uint64_t> hb(nwords);
+                if (own(s, l)) {
+                    KH_HIP(hipStreamSynchronize(G->shards[l]->stream));
+                    KH_HIP(hipMemcpy(hb.data(), d_words[0], nwords * 8, hipMemcpyDeviceToHost));
+                }
+                host_rc(G->tp.broadcast(G->tp.ctx, hb.data(), nwords * 8, s), "broadcast");
+                if (!own(s, l)) {
+                    KH_HIP(hipStreamSynchronize(lc.st_x));
+                    ensure((void **)&lc.slot[b], &lc.cap_slot[b], nwords, 8);
+                    KH_HIP(hipMemcpyAsync(lc.slot[b], hb.data(), nwords * 8, hipMemcpyHostToDevice, lc.st_x));
+                    KH_HIP(hipStreamSynchronize(lc.st_x));
+                }
+            } else if (own(s, l)) {
                 uint64_t *w = const_cast<uint64_t *>(d_words[0]);
                 KH_NCCL(ncclBroadcast(w, w, nwords, ncclUint64, s, G->comm_b, lc.st_x));
             } else {
@@ -1727,11 +1829,11 @@ void group_counters(ShardGroup *G, uint64_t *n_unique, uint64_t *n_occupied) {
         h[0] += g->n_unique;
         h[1] += g->n_occupied;
     }
-    if (G->comm) {
+    if (per_rank(G)) {
         Graph *g = G->shards[0];
         KH_HIP(hipSetDevice(g->device));
         KH_HIP(hipMemcpyAsync(G->d_red + 150, h, 16, hipMemcpyHostToDevice, g->stream));
-        KH_NCCL(ncclAllReduce(G->d_red + 150, G->d_red + 152, 2, ncclUint64, ncclSum, G->comm, g->stream));
+        coll_allreduce_u64(G, g->stream, G->d_red + 150, G->d_red + 152, 2, RED_SUM);
         KH_HIP(hipMemcpyAsync(h, G->d_red + 152, 16, hipMemcpyDeviceToHost, g->stream));
         KH_HIP(hipStreamSynchronize(g->stream));
     }

@@ -255,6 +255,9 @@ struct ShardGroup;
 void group_unique_id(unsigned char *out, size_t n);
 ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank, int nlocal,
                          const int *devices, const unsigned char *uid);
+ShardGroup *group_create_hosted(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank,
+                                int device, const kh_transport *t);
+void group_comm_info(ShardGroup *G, int *nranks, int *device);
 void group_destroy(ShardGroup *G);
 void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len);
 void group_counters(ShardGroup *G, uint64_t *n_unique, uint64_t *n_occupied);

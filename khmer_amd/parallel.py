@@ -12,11 +12,15 @@ k-mer and applies only the updates of the bins it owns (owner-computes), so
 the tables are exactly the single-device tables.  n_unique / n_occupied /
 bigcounts stay exact (see include/khmer_hip.h, kh_group_*).
 
-Process model: one process per GPU under torchrun; torch.distributed (gloo)
-only carries the RCCL unique id, barriers and the max-over-ranks timing; the
-data path is the library's own RCCL communicator.  `loopback=True` runs all
-shards in one process on one device (device copies instead of RCCL), which is
-how the protocol is exercised on a one-GPU box.
+Process model: one process per GPU (torchrun or any launcher that sets
+RANK / WORLD_SIZE / MASTER_ADDR); a small TCP rendezvous
+(khmer_amd.rendezvous, no PyTorch) carries the RCCL unique id, barriers and
+the max-over-ranks timing; the data path is the library's own RCCL
+communicator.  Two other transports run the same protocol where RCCL cannot:
+`loopback=True` holds every shard in one process on one device (device
+copies), and `transport=HostTransport(rendezvous)` keeps one shard per
+process but routes the collectives through host memory and the rendezvous
+(several processes sharing one GPU, as on the one-GPU test box).
 """
 import ctypes
 
@@ -88,21 +92,89 @@ class _ShardView(object):
         return bytes(buf[:n.value])
 
 
+_AG = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+_BC = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int)
+_A2A = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                        ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
+
+
+class _KhTransport(ctypes.Structure):   # include/khmer_hip.h kh_transport
+    _fields_ = [("ctx", ctypes.c_void_p), ("allgather", _AG), ("broadcast", _BC), ("alltoallv", _A2A)]
+
+
+class HostTransport(object):
+    """kh_transport over a rendezvous (khmer_amd.rendezvous.Rendezvous or any
+    object with allgather / broadcast / alltoallv of byte strings)."""
+
+    def __init__(self, rdv):
+        self.rdv = rdv
+        self.error = None
+        world = rdv.world
+
+        def allgather(ctx, send, recv, nbytes):
+            try:
+                parts = rdv.allgather(ctypes.string_at(send, nbytes) if nbytes else b"")
+                ctypes.memmove(recv, b"".join(parts), nbytes * world)
+                return 0
+            except Exception as e:   # reported to the library as a failed collective
+                self.error = e
+                return 1
+
+        def broadcast(ctx, buf, nbytes, root):
+            try:
+                data = rdv.broadcast(ctypes.string_at(buf, nbytes) if rdv.rank == root else b"", root)
+                if rdv.rank != root:
+                    ctypes.memmove(buf, data, nbytes)
+                return 0
+            except Exception as e:
+                self.error = e
+                return 1
+
+        def alltoallv(ctx, send, send_bytes, recv, recv_bytes):
+            try:
+                blocks, at = [], 0
+                for d in range(world):
+                    n = send_bytes[d]
+                    blocks.append(ctypes.string_at(send + at, n) if n else b"")
+                    at += n
+                got = rdv.alltoallv(blocks)
+                at = 0
+                for s in range(world):
+                    n = recv_bytes[s]
+                    if len(got[s]) != n:
+                        raise ValueError("alltoallv: %d bytes from rank %d, expected %d" % (len(got[s]), s, n))
+                    if n:
+                        ctypes.memmove(recv + at, got[s], n)
+                    at += n
+                return 0
+            except Exception as e:
+                self.error = e
+                return 1
+
+        self._fns = (_AG(allgather), _BC(broadcast), _A2A(alltoallv))
+        self.struct = _KhTransport(None, *self._fns)
+
+
 class ShardedGraph(object):
     """A Countgraph/Nodegraph/SmallCountgraph split over `world` ranks."""
 
-    def __init__(self, cls, k, sizes, world, rank=0, device=0, loopback=False, uid=None):
+    def __init__(self, cls, k, sizes, world, rank=0, device=0, loopback=False, uid=None, transport=None):
         self._h = None
         self.shards = []
         self.kind = KIND[cls]
         self.k, self.sizes, self.world = k, [int(x) for x in sizes], world
         self.loopback = loopback
+        self.transport = transport
         nlocal = world if loopback else 1
         devs = (ctypes.c_int * nlocal)(*([device] * nlocal))
         arr = (ctypes.c_uint64 * len(sizes))(*self.sizes)
         h = ctypes.c_void_p()
-        check(lib.kh_group_create(self.kind, _lib.HASH_TWOBIT, k, arr, len(sizes), world, rank, nlocal, devs,
-                                  uid, ctypes.byref(h)))
+        if transport is not None:
+            check(lib.kh_group_create_hosted(self.kind, _lib.HASH_TWOBIT, k, arr, len(sizes), world, rank, device,
+                                             ctypes.byref(transport.struct), ctypes.byref(h)))
+        else:
+            check(lib.kh_group_create(self.kind, _lib.HASH_TWOBIT, k, arr, len(sizes), world, rank, nlocal, devs,
+                                      uid, ctypes.byref(h)))
         self._h = h
         w, nl, r0 = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(lib.kh_group_info(h, ctypes.byref(w), ctypes.byref(nl), ctypes.byref(r0)))
@@ -127,6 +199,12 @@ class ShardedGraph(object):
         buf = ctypes.create_string_buffer(128)
         check(lib.kh_group_unique_id(buf, 128))
         return buf.raw
+
+    def comm_info(self):
+        """(nranks, device) as RCCL reports them (0, -1 without RCCL)."""
+        n, d = ctypes.c_int(), ctypes.c_int()
+        check(lib.kh_group_comm_info(self._h, ctypes.byref(n), ctypes.byref(d)))
+        return n.value, d.value
 
     def slice(self, l, table):
         lo, n = ctypes.c_uint64(), ctypes.c_uint64()
@@ -165,13 +243,18 @@ class ShardedGraph(object):
         """[[slice bytes per table] per local shard]."""
         return [[s.table_bytes(i) for i in range(len(self.sizes))] for s in self.shards]
 
-    def gather_tables(self, all_gather=None):
+    def gather_tables(self, rdv=None):
         """Reference-layout table bytes of the whole group.  Loopback: from the
-        local shards; one-process-per-rank: `all_gather(obj) -> [obj per rank]`
-        (e.g. a torch.distributed gloo all_gather_object wrapper)."""
-        parts = self.local_tables()
-        if not self.loopback:
-            parts = [p[0] for p in all_gather(parts)]
+        local shards; one process per rank: every rank's slices through the
+        rendezvous `rdv` (khmer_amd.rendezvous.Rendezvous)."""
+        if self.loopback:
+            parts = self.local_tables()
+        else:
+            mine = self.local_tables()[0]
+            parts = [[] for _ in range(self.world)]
+            for i in range(len(self.sizes)):
+                for r, blob in enumerate(rdv.allgather(mine[i])):
+                    parts[r].append(blob)
         return [reinterleave(self.kind, p, [parts[r][i] for r in range(self.world)])
                 for i, p in enumerate(self.sizes)]
 
@@ -188,15 +271,15 @@ class ShardedCountgraphBench(object):
             a.k, a.tables, a.x, self.world, a.reads, a.read_len)
 
     def setup(self):
-        import torch.distributed as dist
         from . import synth
+        from .rendezvous import Rendezvous
         a = self.args
-        if not dist.is_initialized():
-            dist.init_process_group("gloo")
-        self.dist = dist
-        obj = [ShardedGraph.unique_id() if self.rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device, uid=obj[0])
+        self.rdv = Rendezvous(self.rank, self.world)
+        uid = self.rdv.broadcast(ShardedGraph.unique_id() if self.rank == 0 else b"", 0)
+        self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device, uid=uid)
+        nranks, dev = self.g.comm_info()
+        self.comm = [tuple(int(x) for x in p.split(b",")) for p in
+                     self.rdv.allgather(b"%d,%d,%d" % (self.rank, nranks, dev))]
         if a.bigcount:
             self.g.set_use_bigcount(True)
         self.g.set_batch_kmers(a.batch_kmers)
@@ -216,13 +299,14 @@ class ShardedCountgraphBench(object):
         check(lib.kh_device_synchronize(self.device))
 
     def barrier(self):
-        self.dist.barrier()
+        self.rdv.barrier()
 
     def max_over_ranks(self, t):
-        import torch
-        x = torch.tensor([t], dtype=torch.float64)
-        self.dist.all_reduce(x, op=self.dist.ReduceOp.MAX)
-        return float(x.item())
+        return self.rdv.max(t)
+
+    def rccl_info(self):
+        """RCCL's own view: nranks and device of every rank."""
+        return {"nranks": sorted({c[1] for c in self.comm}), "devices": [c[2] for c in self.comm]}
 
     def profile(self, on):
         self.g.set_profiling(on)
@@ -245,4 +329,5 @@ class ShardedCountgraphBench(object):
         lib.kh_device_free(self.device, self.words)
         lib.kh_device_free(self.device, self.koff)
         self.g.close()
+        self.rdv.close()
 

@@ -1,0 +1,109 @@
+"""The one-process-per-rank sharding protocol, multi-process, on one GPU.
+
+RCCL refuses two ranks on one device, so here every rank is its own process
+whose group runs the host transport (kh_group_create_hosted): the same
+per-rank code path as the RCCL build -- every collective of
+group_consume_fixed / group_route_winners / group_merge_full / group_counters
+in the same order -- with each collective staged through host memory and the
+TCP rendezvous (khmer_amd.rendezvous) instead of xGMI.  Rank s's reads are the
+s-th block of the synthetic stream; the oracle consumes the concatenation.
+Tables (re-interleaved from every rank's slices), n_unique, n_occupied and
+the replicated bigcount maps must equal the oracle's exactly."""
+import ctypes
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+KINDS = {"Countgraph": 1, "Nodegraph": 2, "SmallCountgraph": 7}
+
+
+def _rank_main():
+    """Body of one rank (run as a subprocess by the test)."""
+    sys.path.insert(0, ROOT)
+    from khmer_amd import parallel, synth, _lib
+    from khmer_amd._lib import lib, check
+    from khmer_amd.rendezvous import Rendezvous
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    cfg = json.loads(os.environ["KH_MP_CFG"])
+    _lib.set_default_device(0)
+    rdv = Rendezvous(rank, world, "127.0.0.1", int(os.environ["KH_RDV_PORT"]), timeout=120)
+    tp = parallel.HostTransport(rdv)
+    g = parallel.ShardedGraph(cfg["cls"], cfg["k"], cfg["sizes"], world, rank, 0, transport=tp)
+    g.set_batch_kmers(cfg["batch"])
+    if cfg["bigcount"]:
+        g.set_use_bigcount(True)
+    n, L, k = cfg["nreads"], cfg["L"], cfg["k"]
+    words, koff = ctypes.c_void_p(), ctypes.c_void_p()
+    check(lib.kh_device_malloc(0, (n * L // 32 + 2) * 8, ctypes.byref(words)))
+    check(lib.kh_device_malloc(0, (n + 1) * 8, ctypes.byref(koff)))
+    check(lib.kh_synth_packed_device(0, synth.SEED, rank * n, n, L, k, words, koff))
+    g.consume_packed_fixed_device([words], n, L)
+    u, occ = g.counters()
+    tabs = g.gather_tables(rdv)
+    bc = g.shards[0].bigcounts()
+    out = {"rank": rank, "n_unique": u, "n_occupied": occ, "bigcounts": [[int(a), int(b)] for a, b in bc],
+           "comm": g.comm_info()}
+    if rank == 0:
+        import hashlib
+        out["tables"] = [hashlib.sha256(t).hexdigest() for t in tabs]
+    print("RESULT " + json.dumps(out), flush=True)
+    lib.kh_device_free(0, words)
+    lib.kh_device_free(0, koff)
+    g.close()
+    rdv.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("cls,world,bigcount", [("Countgraph", 2, True), ("Countgraph", 3, True),
+                                                ("Nodegraph", 2, False), ("SmallCountgraph", 3, False)])
+def test_hosted_group_multiprocess(cls, world, bigcount):
+    import hashlib
+    from oracle import oracle as O
+    from khmer_amd import synth
+    sizes = O.get_n_primes_near_x(4, 100003)
+    cfg = {"cls": cls, "k": 21, "sizes": sizes, "batch": 1 << 20, "bigcount": bigcount, "nreads": 20000, "L": 150}
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), KH_RDV_PORT=str(port), KH_MP_CFG=json.dumps(cfg))
+        procs.append(subprocess.Popen([sys.executable, "-c", "import tests.test_gpu_shard_mp as t; t._rank_main()"],
+                                      cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = []
+    for p in procs:
+        try:
+            so, _ = p.communicate(timeout=180)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, so[-3000:]
+        outs.append(json.loads([ln for ln in so.splitlines() if ln.startswith("RESULT ")][-1][7:]))
+    o = O.Table(KINDS[cls], 21, sizes)
+    o.set_use_bigcount(bigcount)
+    for s in range(world):
+        seqs, offs = synth.batch(s * cfg["nreads"], cfg["nreads"], cfg["L"])
+        o.consume_batch(seqs, [int(v) for v in offs])
+    r0 = [x for x in outs if x["rank"] == 0][0]
+    assert r0["tables"] == [hashlib.sha256(o.table_bytes(i)).hexdigest() for i in range(len(sizes))]
+    ref_bc = sorted([int(a), int(b)] for a, b in o.bigcounts().items())
+    for x in outs:
+        assert (x["n_unique"], x["n_occupied"]) == (o.n_unique_kmers(), o.n_occupied())
+        assert x["bigcounts"] == ref_bc
+        assert x["comm"] == [0, -1]   # no RCCL in a host-transport group
+    if bigcount:
+        assert ref_bc, "the case should exercise the bigcount merge"
