@@ -43,7 +43,10 @@ def _rank_main():
     words, koff = ctypes.c_void_p(), ctypes.c_void_p()
     check(lib.kh_device_malloc(0, (n * L // 32 + 2) * 8, ctypes.byref(words)))
     check(lib.kh_device_malloc(0, (n + 1) * 8, ctypes.byref(koff)))
-    check(lib.kh_synth_packed_device(0, synth.SEED, rank * n, n, L, k, words, koff))
+    if cfg["genome"]:
+        check(lib.kh_synth_genomic_device(0, synth.SEED, cfg["genome"], rank * n, n, L, k, words, koff))
+    else:
+        check(lib.kh_synth_packed_device(0, synth.SEED, rank * n, n, L, k, words, koff))
     g.consume_packed_fixed_device([words], n, L)
     u, occ = g.counters()
     tabs = g.gather_tables(rdv)
@@ -75,7 +78,11 @@ def test_hosted_group_multiprocess(cls, world, bigcount):
     from oracle import oracle as O
     from khmer_amd import synth
     sizes = O.get_n_primes_near_x(4, 100003)
-    cfg = {"cls": cls, "k": 21, "sizes": sizes, "batch": 1 << 20, "bigcount": bigcount, "nreads": 20000, "L": 150}
+    # bigcount cases read a 6 kbp genome (every k-mer ~400x, past 255 in all
+    # tables); the others the iid stream
+    genome = 6000 if bigcount else 0
+    cfg = {"cls": cls, "k": 21, "sizes": sizes, "batch": 1 << 20, "bigcount": bigcount, "nreads": 20000, "L": 150,
+           "genome": genome}
     port = _free_port()
     procs = []
     for r in range(world):
@@ -96,7 +103,10 @@ def test_hosted_group_multiprocess(cls, world, bigcount):
     o = O.Table(KINDS[cls], 21, sizes)
     o.set_use_bigcount(bigcount)
     for s in range(world):
-        seqs, offs = synth.batch(s * cfg["nreads"], cfg["nreads"], cfg["L"])
+        if genome:
+            seqs, offs = synth.genomic_batch(s * cfg["nreads"], cfg["nreads"], cfg["L"], genome)
+        else:
+            seqs, offs = synth.batch(s * cfg["nreads"], cfg["nreads"], cfg["L"])
         o.consume_batch(seqs, [int(v) for v in offs])
     r0 = [x for x in outs if x["rank"] == 0][0]
     assert r0["tables"] == [hashlib.sha256(o.table_bytes(i)).hexdigest() for i in range(len(sizes))]
