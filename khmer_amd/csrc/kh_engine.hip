@@ -183,6 +183,9 @@ static void ensure_recs(Graph *g, uint64_t recs) {
 
 // ---- fixed-capacity level 2 (k_scatter_l2f) ----
 // Workgroups per level-1 bucket: enough for ~2048 in the grid.
+static int env_seg(const char *name, int dflt);
+static int l1f_blk_sh() { static const int v = env_seg("KH_L1F_BLK_SH", L1F_BLK_SH); return v; }
+static int l2f_blk_sh() { static const int v = env_seg("KH_L2F_BLK_SH", L2F_BLK_SH); return v; }
 static uint32_t l2f_parts(uint32_t F1) { return std::max<uint32_t>(1, std::min<uint32_t>(16, (2048 + F1 - 1) / F1)); }
 static size_t lds_scatter_l2f(const Params &P) { return ((size_t)1 << P.s2) * (8 + 8 + 16 * 8 + 4 + 4); }
 
@@ -209,7 +212,7 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
     if (w.reg_base && w.reg_nkmers == nkmers) return w.reg_total;
     const uint64_t nreg = (uint64_t)P.F1 << P.s2;
     const uint64_t R = 1ull << P.s0;
-    const uint64_t slack = (uint64_t)(l2f_parts(P.F1) + 1) * L2F_BLK + 16;
+    const uint64_t slack = (uint64_t)(l2f_parts(P.F1) + 1) * (1ull << l2f_blk_sh()) + 16;
     std::vector<uint64_t> base(nreg + 1, 0);
     uint64_t acc = 0;
     int i = 0;
@@ -260,21 +263,41 @@ static uint32_t device_cus(const Graph *g) {
 }
 // a persistent grid: two workgroups per CU (the kernel's LDS allows two at up
 // to ~512 buckets), fewer for small passes
-static uint32_t l1f_wpc() { static const int v = env_seg("KH_L1F_WPC", 2); return (uint32_t)std::max(1, v); }
-static uint32_t l1f_workgroups(const Graph *g, uint64_t nkmers) {
-    const uint64_t tiles = (nkmers + L1_THREADS - 1) / L1_THREADS;
-    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles / 8 + 1, (uint64_t)l1f_wpc() * device_cus(g)));
-}
+// records per thread and tile: 8 (3 workgroups per CU) or 16 (2 workgroups,
+// twice the tile); KH_L1F_RPT (development)
+static int l1f_rpt() { static const int v = env_seg("KH_L1F_RPT", L1_MAX_RPT) == 16 ? 16 : L1_MAX_RPT; return v; }
 static size_t lds_scatter_l1f(const Params &P, bool window, int tile_kmers) {
     const size_t F1a = (P.F1 + 3) & ~3u;
-    const size_t tile = (size_t)L1_THREADS * L1_MAX_RPT;
-    return F1a * 8 * 5 + tile * 8 + F1a * 4 * 5 + tile * 2 + 64 + lds_window(window, tile_kmers);
+    const size_t tile = (size_t)L1_THREADS * l1f_rpt();
+    return F1a * 8 * 5 + tile * 4 + F1a * 4 * 5 + tile * 2 * 2 + 64 + lds_window(window, tile_kmers);
+}
+// as many workgroups per CU as the LDS allows, up to the kernel's register
+// budget (3 at 8 records per thread, 2 at 16); KH_L1F_WPC overrides (development)
+static uint32_t l1f_wpc(const Params &P) {
+    static const int v = env_seg("KH_L1F_WPC", 0);
+    if (v > 0) return (uint32_t)v;
+    const size_t lds = lds_scatter_l1f(P, false, L1_THREADS * l1f_rpt());
+    const size_t regs = (l1f_rpt() == 8 ? L1F_WAVES_PER_EU : 4) * 4 / (L1_THREADS / 64);
+    return (uint32_t)std::max<size_t>(1, std::min<size_t>(regs, 163840 / lds));
+}
+static uint32_t l1f_workgroups(const Graph *g, uint64_t nkmers) {
+    const uint64_t tiles = (nkmers + L1_THREADS - 1) / L1_THREADS;
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles / 8 + 1, (uint64_t)l1f_wpc(g->prm) * device_cus(g)));
 }
 template <class Src>
 using L1FFn = void (*)(Params, Src, uint64_t, uint64_t, int, int, const uint64_t *, unsigned long long *, uint64_t *,
-                       uint64_t *);
+                       uint64_t *, int);
 template <class Src>
-static L1FFn<Src> l1f_kernel(int kpt) {
+static L1FFn<Src> l1f_kernel(int kpt, int rpt) {
+    if (rpt == 16) {
+        switch (kpt) {
+            case 1: return k_scatter_l1f<Src, 1, 16>;
+            case 2: return k_scatter_l1f<Src, 2, 16>;
+            case 4: return k_scatter_l1f<Src, 4, 16>;
+            case 8: return k_scatter_l1f<Src, 8, 16>;
+            default: return k_scatter_l1f<Src, 16, 16>;
+        }
+    }
     switch (kpt) {
         case 1: return k_scatter_l1f<Src, 1>;
         case 2: return k_scatter_l1f<Src, 2>;
@@ -290,7 +313,7 @@ static uint64_t bkt_plan(Graph *g, uint64_t nkmers) {
     const Params &P = g->prm;
     if (w.bkt_base && w.bkt_nkmers == nkmers) return w.bkt_total;
     const uint64_t F1 = P.F1, span = 1ull << (P.s0 + P.s2);
-    const uint64_t slack = (uint64_t)l1f_workgroups(g, nkmers) * L1F_BLK + 16;
+    const uint64_t slack = (uint64_t)l1f_workgroups(g, nkmers) * (1ull << l1f_blk_sh()) + 16;
     std::vector<uint64_t> base(F1 + 1, 0);
     uint64_t acc = 0;
     int i = 0;
@@ -626,18 +649,21 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
         // level 1
         if (l1f) {
             ensure_recs(g, std::max(cap1, cap2));
+            if (P.ablate & 16) KH_HIP(hipMemsetAsync(w.rec1, 0xFF, w.cap_recs * 8, st));   // timing only
             hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)((F1 + 255) / 256)), dim3(256), 0, st, w.bkt_base,
                                (unsigned long long *)w.bkt_cur, (uint64_t)F1);
             const uint32_t nwg = l1f_workgroups(g, nkmers);
             for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
                 const int nt = std::min(L1_MAX_RPT, P.n - t0);
-                const int kpt = std::max(1, L1_MAX_RPT / nt);
+                const int rpt = l1f_rpt();
+                int kpt = 1;
+                while (kpt * 2 * nt <= rpt) kpt *= 2;
                 const uint64_t tk = (uint64_t)L1_THREADS * kpt;
                 const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
-                TIMED("scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt), dim3(nwg), dim3(L1_THREADS),
+                TIMED("scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt), dim3(nwg), dim3(L1_THREADS),
                                                        lds_scatter_l1f(P, window, (int)tk), st, P, src, nkmers, kpw,
                                                        t0, nt, w.bkt_base, (unsigned long long *)w.bkt_cur, w.rec1,
-                                                       w.ctr));
+                                                       w.ctr, l1f_blk_sh()));
             }
         } else if (use_own_filter(g)) {
             nrec = own_filter(g, src, nkmers, window);
@@ -693,10 +719,11 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                                st, w.reg_base, (unsigned long long *)w.reg_cur, nreg);
             const uint64_t *bs = l1f ? w.bkt_base : w.off1;
             const uint64_t *be = l1f ? w.bkt_cur : w.off1 + 1;
-            TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(F1 * parts)),
+            static const int l2rpt = env_seg("KH_L2_RPT", L2_RPT);   // development: 8 or 16
+            TIMED("scatter_l2", hipLaunchKernelGGL((l2rpt == 16 ? k_scatter_l2f<PT_THREADS, 16> : k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(F1 * parts)),
                                                    dim3(PT_THREADS), lds_scatter_l2f(P), st, (uint32_t)F1, P.s0, P.s2,
                                                    parts, bs, be, w.reg_base, (unsigned long long *)w.reg_cur, w.rec1,
-                                                   w.rec2, w.ctr));
+                                                   w.rec2, w.ctr, l2f_blk_sh()));
             uint64_t err = 0;
             KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
             KH_HIP(hipStreamSynchronize(st));
@@ -1189,6 +1216,8 @@ void graph_prepare_params(Graph *g) {
     }
     const int half = (ceil_log2(std::max<uint64_t>(nreg, 1)) + 1) / 2;
     P.s2 = std::min({10, ceil_log2(maxreg), std::max(half + 1, 1)});
+    static const int s2_env = env_seg("KH_S2", 0);   // development: force the level-2 fan-out
+    if (s2_env > 0) P.s2 = std::min({10, s2_env, std::max(ceil_log2(maxreg), 1)});
     const uint64_t span = 1ull << (P.s0 + P.s2);
     uint64_t base = 0, byteoff = 0;
     for (int i = 0; i < g->n; i++) {
@@ -1228,15 +1257,17 @@ static void set_lds_limits() {
             KH_LDS_MAX(l1_kernel<SrcHashes>(seg, kpt));
         }
     KH_LDS_MAX((k_scatter_l2<PT_THREADS, 2, L2_RPT>));
+    KH_LDS_MAX((k_scatter_l2f<PT_THREADS, 16>));
     KH_LDS_MAX((k_scatter_l2<PT_THREADS, 4, L2_RPT>));
     KH_LDS_MAX((k_scatter_l2<PT_THREADS, 8, L2_RPT>));
     KH_LDS_MAX((k_scatter_l2<PT_THREADS, 16, L2_RPT>));
     KH_LDS_MAX((k_scatter_l2f<PT_THREADS, L2_RPT>));
-    for (int kpt : {1, 2, 4, 8}) {
-        KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt));
-        KH_LDS_MAX(l1f_kernel<SrcBytes>(kpt));
-        KH_LDS_MAX(l1f_kernel<SrcHashes>(kpt));
-    }
+    for (int kpt : {1, 2, 4, 8, 16})
+        for (int rpt : {8, 16}) {
+            KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt, rpt));
+            KH_LDS_MAX(l1f_kernel<SrcBytes>(kpt, rpt));
+            KH_LDS_MAX(l1f_kernel<SrcHashes>(kpt, rpt));
+        }
     KH_LDS_MAX((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 1>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 2>));

@@ -437,18 +437,22 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
 // bucket b's records are then [bkt_base[b], bkt_cur[b]).  A bucket that runs
 // out of capacity sets ctr[CTR_ERR] bit 8 and the host redoes the pass with
 // the exact two-pass level 1.
-constexpr uint32_t L1F_BLK = 256;
+constexpr int L1F_BLK_SH = 8;   // default block: 256 records (KH_L1F_BLK_SH)
+// 3 workgroups of 8 waves per CU: <= 80 VGPRs, ~47 KB of LDS at F1 <= 256
+#ifndef L1F_WAVES_PER_EU
+#define L1F_WAVES_PER_EU 6
+#endif
 
-template <class Src, int KPT>
-__global__ void __launch_bounds__(L1_THREADS) k_scatter_l1f(Params P, Src src, uint64_t nkmers, uint64_t kpw, int t0,
+template <class Src, int KPT, int RPT_ = L1_MAX_RPT>
+__global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) k_scatter_l1f(Params P, Src src, uint64_t nkmers, uint64_t kpw, int t0,
                                                            int nt, const uint64_t *bkt_base,
                                                            unsigned long long *bkt_cur, uint64_t *rec,
-                                                           uint64_t *ctr) {
+                                                           uint64_t *ctr, int blk_sh) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int RPT = L1_MAX_RPT;
+    constexpr int RPT = RPT_;
     constexpr int TILE_RECS = L1_THREADS * RPT;
     constexpr int TILE_KMERS = L1_THREADS * KPT;
-    constexpr uint32_t BLK = L1F_BLK;
+    const uint32_t BLK = 1u << blk_sh;
     constexpr uint64_t DEAD = ~0ull;
     const uint32_t F1 = P.F1;
     const uint32_t F1a = (F1 + 3) & ~3u;
@@ -456,15 +460,16 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1f(Params P, Src src, u
     uint64_t *nbase = bcur + F1a;                       // [F1] blocks reserved for this tile
     uint64_t *dla = nbase + F1a;                        // [F1] output - LDS position, current block
     uint64_t *dlb = dla + F1a;                          // [F1] output - LDS position, new blocks
-    uint64_t *stage = dlb + F1a;                        // [TILE_RECS]
-    uint64_t *tail = stage + TILE_RECS;                 // [F1] a pending odd record
-    uint32_t *cnt = (uint32_t *)(tail + F1a);           // [F1] records appended by this workgroup
+    uint64_t *tail = dlb + F1a;                         // [F1] a pending odd record
+    uint32_t *stage = (uint32_t *)(tail + F1a);         // [TILE_RECS] bin offset inside the bucket
+    uint32_t *cnt = stage + TILE_RECS;                  // [F1] records appended by this workgroup
     uint32_t *hist = cnt + F1a;                         // [F1]
     uint32_t *lstart = hist + F1a;                      // [F1]
     uint32_t *qs = lstart + F1a;                        // [F1] first LDS position in the new blocks
     uint32_t *qlim = qs + F1a;                          // [F1] first LDS position left for the tail
-    uint16_t *sb = (uint16_t *)(qlim + F1a);            // [TILE_RECS]
-    uint32_t *s_wtot = (uint32_t *)(sb + TILE_RECS);    // [16]
+    uint16_t *sb = (uint16_t *)(qlim + F1a);            // [TILE_RECS] bucket
+    uint16_t *sj = sb + TILE_RECS;                      // [TILE_RECS] k-mer index inside the tile
+    uint32_t *s_wtot = (uint32_t *)(sj + TILE_RECS);    // [16]
     uint64_t *s_meta = (uint64_t *)(s_wtot + 16);
     uint64_t *s_koff = s_meta + 2;
     const int shift = P.s0 + P.s2;
@@ -492,17 +497,18 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1f(Params P, Src src, u
         const bool last = ti + 1 == ntiles;
         block_sync();
         TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
-        uint64_t G[RPT];
-        uint32_t rank[RPT];
-        uint32_t jj[RPT];
-        int nr = 0;
+        // per record slot q (k-mer a = q / nt of this thread): bin offset
+        // inside its bucket (~0: none) and (a << 23 | bucket << 13 | tile
+        // rank); the k-mer index is j0 + a * L1_THREADS + thread: 2 VGPRs per record
+        uint32_t off[RPT], br[RPT];
 #pragma unroll
-        for (int q = 0; q < RPT; q++) { G[q] = ~0ull; rank[q] = 0; jj[q] = 0; }
+        for (int q = 0; q < RPT; q++) { off[q] = ~0u; br[q] = 0; }
         uint64_t hh[KPT];
 #pragma unroll
         for (int a = 0; a < KPT; a++) {
             const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
             hh[a] = j < j1 ? (pre ? src.finish(pend[a]) : kmer_hash(src, s_koff, tr, j)) : 0;
+            if (P.ablate & 32) hh[a] = (j * 0x9E3779B97F4A7C15ull) >> 22;   // timing only: no fetch/hash
         }
 #pragma unroll
         for (int a = 0; a < KPT; a++) {
@@ -514,10 +520,9 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1f(Params P, Src src, u
                 if (ok && i >= 0 && i < nt) {
                     uint64_t Gq;
                     if (local_bin(P, t0 + i, hh[a], &Gq)) {
-                        G[q] = Gq;
-                        jj[q] = (uint32_t)j;
-                        rank[q] = atomicAdd(&hist[(uint32_t)(Gq >> shift)], 1u);
-                        nr = q + 1;
+                        const uint32_t b = (uint32_t)(Gq >> shift);
+                        off[q] = (uint32_t)(Gq & omask);
+                        br[q] = ((uint32_t)a << 23) | (b << 13) | atomicAdd(&hist[b], 1u);
                     }
                 }
             }
@@ -527,11 +532,12 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1f(Params P, Src src, u
         block_sync();
 #pragma unroll
         for (int q = 0; q < RPT; q++) {
-            if (q < nr && G[q] != ~0ull) {
-                const uint32_t b = (uint32_t)(G[q] >> shift);
-                const uint32_t pos = lstart[b] + rank[q];
-                stage[pos] = ((uint64_t)jj[q] << 32) | (G[q] & omask);
+            if (off[q] != ~0u) {
+                const uint32_t b = (br[q] >> 13) & 1023u;
+                const uint32_t pos = lstart[b] + (br[q] & 8191u);
+                stage[pos] = off[q];
                 sb[pos] = (uint16_t)b;
+                sj[pos] = (uint16_t)((br[q] >> 23) * L1_THREADS + threadIdx.x);
             }
         }
         if (pre) {
@@ -539,7 +545,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1f(Params P, Src src, u
 #pragma unroll
             for (int a = 0; a < KPT; a++) {
                 const uint64_t j = n0 + (uint64_t)a * L1_THREADS + threadIdx.x;
-                if (j < n1) pend[a] = kmer_fetch(src, j);
+                if (j < n1 && !(P.ablate & 32)) pend[a] = kmer_fetch(src, j);
             }
         }
         // per bucket: block reservation (one atomic when the tile needs new
@@ -550,7 +556,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1f(Params P, Src src, u
             if (!h && !last) continue;
             const uint32_t L0 = cnt[d];
             const uint32_t split = (L0 + BLK - 1) & ~(BLK - 1);
-            const uint32_t need = (L0 + h + BLK - 1) / BLK - split / BLK;
+            const uint32_t need = ((L0 + h + BLK - 1) >> blk_sh) - (split >> blk_sh);
             uint64_t bc = bcur[d], nb = 0;
             if (bc == DEAD) {
                 nb = DEAD;
@@ -578,15 +584,18 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1f(Params P, Src src, u
             const uint32_t q = threadIdx.x + (uint32_t)u * L1_THREADS;
             if (q >= ntile) continue;
             const uint32_t d = sb[q];
-            if (q < qlim[d]) rec[(q < qs[d] ? dla[d] : dlb[d]) + q] = stage[q];
-            else tail[d] = stage[q];   // the odd last record of the run (not on the last tile)
+            const uint64_t v = ((j0 + sj[q]) << 32) | stage[q];
+            if (q < qlim[d]) {
+                if (!(P.ablate & 16)) rec[(q < qs[d] ? dla[d] : dlb[d]) + q] = v;   // 16: timing only, no run writes
+            }
+            else tail[d] = v;   // the odd last record of the run (not on the last tile)
         }
         block_sync();
         for (uint32_t d = threadIdx.x; d < F1; d += blockDim.x) {
             const uint32_t h = hist[d];
             if (!h) continue;
             const uint32_t L0 = cnt[d];
-            const uint32_t need = (L0 + h + BLK - 1) / BLK - (L0 + BLK - 1) / BLK;
+            const uint32_t need = ((L0 + h + BLK - 1) >> blk_sh) - ((L0 + BLK - 1) >> blk_sh);
             if (nbase[d] == DEAD) bcur[d] = DEAD;
             else if (need) bcur[d] = nbase[d] + (uint64_t)(need - 1) * BLK;
             cnt[d] = L0 + h;
@@ -595,7 +604,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1f(Params P, Src src, u
     }
     block_sync();
     for (uint32_t y = threadIdx.x; y < F1 * BLK; y += blockDim.x) {
-        const uint32_t d = y / BLK, sl = y % BLK;
+        const uint32_t d = y >> blk_sh, sl = y & (BLK - 1);
         const uint32_t c = cnt[d] & (BLK - 1);
         if (c == 0 || sl < c || bcur[d] == DEAD) continue;
         rec[bcur[d] + sl] = ~0ull;
@@ -871,7 +880,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2(uint32_t F1, int s0, int
 // [reg_base[g], reg_cur[g]).  A reservation past the region's capacity (a
 // skewed input) sets ctr[CTR_ERR] bit 4, writes nothing for that region, and
 // the host redoes the pass's level 2 with the exact histogram path.
-constexpr uint32_t L2F_BLK = 64;
+constexpr int L2F_BLK_SH = 6;   // default block: 64 records (KH_L2F_BLK_SH)
 constexpr uint64_t L2F_DEAD = ~0ull;
 
 template <int THREADS, int RPT>
@@ -879,9 +888,10 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
                                                          const uint64_t *bstart, const uint64_t *bend,
                                                          const uint64_t *reg_base,
                                                          unsigned long long *reg_cur, const uint64_t *rec_in,
-                                                         uint64_t *rec_out, uint64_t *ctr) {
+                                                         uint64_t *rec_out, uint64_t *ctr, int blk_sh) {
     constexpr int TILE = THREADS * RPT;
-    constexpr uint32_t SEG = 16, BLK = L2F_BLK;
+    constexpr uint32_t SEG = 16;
+    const uint32_t BLK = 1u << blk_sh;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t F2 = 1u << s2;
     uint64_t *bcur = (uint64_t *)smem;              // [F2] base of the partially filled block (DEAD: overflowed)
@@ -938,7 +948,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
             const uint32_t h = hist[d], c0 = cnt[d];
             uint64_t nb = 0;
             if (h) {
-                const uint32_t need = (c0 + h + BLK - 1) / BLK - (c0 + BLK - 1) / BLK;
+                const uint32_t need = ((c0 + h + BLK - 1) >> blk_sh) - ((c0 + BLK - 1) >> blk_sh);
                 if (bcur[d] == L2F_DEAD) {
                     nb = L2F_DEAD;
                 } else if (need) {
@@ -983,7 +993,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
             const uint32_t h = hist[d];
             if (!h) continue;
             const uint32_t c0 = cnt[d];
-            const uint32_t need = (c0 + h + BLK - 1) / BLK - (c0 + BLK - 1) / BLK;
+            const uint32_t need = ((c0 + h + BLK - 1) >> blk_sh) - ((c0 + BLK - 1) >> blk_sh);
             if (nbase[d] == L2F_DEAD) bcur[d] = L2F_DEAD;
             else if (need) bcur[d] = nbase[d] + (uint64_t)(need - 1) * BLK;
             cnt[d] = c0 + h;
@@ -993,7 +1003,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
     // the rest of every partially filled block: sentinels
     block_sync();
     for (uint32_t y = threadIdx.x; y < F2 * BLK; y += THREADS) {
-        const uint32_t d = y / BLK, sl = y % BLK;
+        const uint32_t d = y >> blk_sh, sl = y & (BLK - 1);
         const uint32_t c = cnt[d] & (BLK - 1);
         if (c == 0 || sl < c || bcur[d] == L2F_DEAD) continue;
         rec_out[bcur[d] + sl] = ~0ull;
