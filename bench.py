@@ -41,10 +41,21 @@ def algorithmic_bytes_per_kmer(L, k, n_tables):
 CONFIGS = {
     "C2": ("Countgraph", 21, 1e9),
     "C3": ("Nodegraph", 31, 4e9),
+    "C4": ("Countgraph", 21, 8e9),
     "C5": ("SmallCountgraph", 31, 8e9),
+    "C5M": ("SmallCounttable", 51, 8e9),
 }
-DTYPE = {"Countgraph": "u8", "Nodegraph": "u1 (bit)", "SmallCountgraph": "u4 (nibble)"}
-ORACLE_KIND = {"Countgraph": "BYTE", "Nodegraph": "BIT", "SmallCountgraph": "NIBBLE"}
+DTYPE = {"Countgraph": "u8", "Nodegraph": "u1 (bit)", "SmallCountgraph": "u4 (nibble)",
+         "SmallCounttable": "u4 (nibble)"}
+ORACLE_KIND = {"Countgraph": "BYTE", "Nodegraph": "BIT", "SmallCountgraph": "NIBBLE", "SmallCounttable": "NIBBLE"}
+MURMUR = {"SmallCounttable"}   # Counttable family: MurmurHash3 over ASCII k-mers
+
+
+def query_bytes_per_kmer(L, k, n_tables):
+    """SURVEY.md §8(d) C5 query: 2-bit input + 1 B read per table + the
+    per-read outputs (u16 median + 2 x f32) spread over the read's k-mers."""
+    kpr = L - k + 1
+    return (L / 4.0) / kpr + 1.0 * n_tables + 10.0 / kpr
 
 
 def parse():
@@ -63,6 +74,13 @@ def parse():
                     help="largest device pass (the library cap, MAX_PASS_KMERS); fewer, larger passes "
                          "amortise the per-bin work of every pass")
     ap.add_argument("--no-bigcount", action="store_true")
+    ap.add_argument("--genome", type=float, default=0,
+                    help="bases of the random genome of the skewed 'genomic' stream (SURVEY.md §8(d): 1e8); "
+                         "0 = iid uniform reads")
+    ap.add_argument("--strong", action="store_true",
+                    help="multi-GPU strong scaling: --reads is the whole job, split over the ranks")
+    ap.add_argument("--query", action="store_true",
+                    help="time get_median_count over the reads (tables built from them first, untimed)")
     ap.add_argument("--ablate", type=int, default=0,
                     help="timing-only KH_ABLATE bits (results become wrong; never for reported numbers)")
     ap.add_argument("--variable-path", action="store_true",
@@ -75,6 +93,8 @@ def parse():
     a.k = k if a.k is None else a.k
     a.x = x if a.x is None else a.x
     a.bigcount = a.graph == "Countgraph" and not a.no_bigcount
+    a.genome = int(a.genome)
+    a.murmur = a.graph in MURMUR
     return a
 
 
@@ -112,65 +132,95 @@ def host_threads():
 
 
 def cpu_baseline(args, sizes):
-    """The oracle (C restatement of Hashtable::consume_string / consume_seqfile,
-    oracle/khmer_oracle.c) on bounded samples of the same synthetic stream into
-    same-size tables, on this host's cores:
-      * in-memory batch, T = host_threads() (the reference's -T N mode: atomic
-        byte updates, src/oxli/hashtable.cc:125-150)  -> `value`
+    """The oracle (C restatement of Hashtable::consume_string / consume_seqfile /
+    get_median_count, oracle/khmer_oracle.c) on bounded samples of the same
+    synthetic stream into same-size tables, on this host's cores:
       * in-memory batch, T = 1 (stream order, the exact semantics)
+      * in-memory batch, T = host_threads() (the reference's -T N mode: atomic
+        byte updates and shared occupancy counter, src/oxli/hashtable.cc:125-150)
       * end to end from a page-cached FASTQ file, T = 1 (parse + clean + count)
-    """
+    `value` is the faster of the two in-memory rates.  --query: the oracle's
+    get_median_count (src/oxli/hashtable.cc:299-328) per read, T = 1, over
+    tables built from the same sample."""
     from oracle import oracle as O
     from khmer_amd import synth
     kind = getattr(O, ORACLE_KIND[args.graph])
+    hashfn = O.MURMUR if args.murmur else O.TWOBIT
     n = args.cpu_reads
     chunk = 100_000
     batches = []
     for r0 in range(0, n, chunk):
-        seqs, offs = synth.batch(r0, min(chunk, n - r0), args.read_len)
+        if args.genome:
+            seqs, offs = synth.genomic_batch(r0, min(chunk, n - r0), args.read_len, args.genome)
+        else:
+            seqs, offs = synth.batch(r0, min(chunk, n - r0), args.read_len)
         batches.append((seqs, [int(v) for v in offs]))
 
-    def run(threads):
-        t = O.Table(kind, args.k, sizes)
+    def table():
+        t = O.Table(kind, args.k, sizes, hashfn)
         t.set_use_bigcount(args.bigcount)
+        return t
+
+    def run(threads):
+        t = table()
         total, secs = 0, 0.0
         for seqs, offs in batches:
             t0 = time.perf_counter()
             total += t.consume_batch(seqs, offs, threads=threads if threads > 1 else 0)
             secs += time.perf_counter() - t0
-        return total, secs
+        return total, secs, t
 
     T = host_threads()
-    k1, s1 = run(1)
-    kT, sT = run(T)
+    k1, s1, t1 = run(1)
+    if args.query:
+        nq = min(n, 200_000)
+        L = args.read_len
+        seqs = batches[0][0] if nq <= chunk else b"".join(b[0] for b in batches)
+        t0 = time.perf_counter()
+        for r in range(nq):
+            t1.median(seqs[r * L:(r + 1) * L])
+        dt = time.perf_counter() - t0
+        kq = nq * (L - args.k + 1)
+        return {
+            "value": kq / dt, "unit": "k-mers/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
+            "sample": "get_median_count over %d synthetic %d bp reads (%d k-mers) of the benchmark stream, tables "
+                      "built from the first %d reads; oracle/khmer_oracle.c, 1 thread" % (nq, L, kq, n),
+        }
+    del t1
+    kT, sT, tT = run(T)
+    del tT
     # end to end: FASTQ in the page cache (written, then read once untimed)
     import tempfile
     nfq = min(n, 500_000)
     e2e = None
-    with tempfile.TemporaryDirectory() as tmp:
-        fq = os.path.join(tmp, "sample.fq")
-        synth.write_fastq(fq, nfq, args.read_len)
-        with open(fq, "rb") as fh:
-            while fh.read(1 << 24):
-                pass
-        t = O.Table(kind, args.k, sizes)
-        t.set_use_bigcount(args.bigcount)
-        t0 = time.perf_counter()
-        _, kmers = t.consume_fastx(fq)
-        e2e = kmers / (time.perf_counter() - t0)
+    if not args.genome:
+        with tempfile.TemporaryDirectory() as tmp:
+            fq = os.path.join(tmp, "sample.fq")
+            synth.write_fastq(fq, nfq, args.read_len)
+            with open(fq, "rb") as fh:
+                while fh.read(1 << 24):
+                    pass
+            t = table()
+            t0 = time.perf_counter()
+            _, kmers = t.consume_fastx(fq)
+            e2e = kmers / (time.perf_counter() - t0)
+            del t
+    r1, rT = k1 / s1, kT / sT
     return {
-        "value": kT / sT,
+        "value": max(r1, rT),
         "unit": "k-mers/s",
-        "cores": T,
+        "cores": 1 if r1 >= rT else T,
         "kind": "port",
         "cpu_model": cpu_model(),
-        "t1_in_memory": k1 / s1,
-        "tN_in_memory": kT / sT,
+        "t1_in_memory": r1,
+        "tN_in_memory": rT,
+        "tN_threads": T,
         "t1_end_to_end_fastq": e2e,
         "sample": "%d synthetic %d bp reads (%d k-mers, the first reads of the benchmark stream) into the same "
-                  "%dx%.0e %s; oracle/khmer_oracle.c: value = %d threads with the reference's -T N atomic "
-                  "updates, t1 = single-threaded stream order, end-to-end = %d reads parsed from a "
-                  "page-cached FASTQ, 1 thread" % (n, args.read_len, k1, args.tables, args.x, args.graph, T, nfq),
+                  "%dx%.0e %s; oracle/khmer_oracle.c: value = the faster of 1 thread (stream order) and %d threads "
+                  "(the reference's -T N atomic updates; its shared occupancy counter serialises them); "
+                  "end-to-end = %d reads parsed from a page-cached FASTQ, 1 thread"
+                  % (n, args.read_len, k1, args.tables, args.x, args.graph, T, nfq),
     }
 
 
@@ -192,8 +242,12 @@ def main():
     _lib.set_default_device(local)
 
     L, k, nt = args.read_len, args.k, args.tables
+    if args.strong and world > 1:
+        args.reads = (args.reads + world - 1) // world   # per rank
     nreads = args.reads
     nkmers = nreads * (L - k + 1)
+    if args.query and world > 1:
+        raise SystemExit("--query runs on one GPU")
     sizes = khmer_amd.get_n_primes_near_x(nt, args.x)
 
     if world > 1:
@@ -219,7 +273,7 @@ def main():
     runner.profile(False)
     check_info = runner.check()
 
-    bpk = algorithmic_bytes_per_kmer(L, k, nt)
+    bpk = query_bytes_per_kmer(L, k, nt) if args.query else algorithmic_bytes_per_kmer(L, k, nt)
     total_kmers = nkmers * world * args.steps
     value = total_kmers / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
@@ -256,8 +310,12 @@ def main():
         cpu = cpu_baseline(args, sizes)
 
     if rank == 0:
+        if args.query:
+            metric = "k-mers queried/sec by get_median_count on %s (k=%d, %dx%.0e)" % (args.graph, k, nt, args.x)
+        else:
+            metric = "k-mers hashed/sec into %s (k=%d, %dx%.0e)" % (args.graph, k, nt, args.x)
         line = {
-            "metric": "k-mers hashed/sec into %s (k=%d, %dx%.0e)" % (args.graph, k, nt, args.x),
+            "metric": metric,
             "value": value,
             "unit": "k-mers/s",
             "n_gpus": world,
@@ -265,21 +323,28 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if (args.strong and world > 1) else "weak",
             "vs_baseline": None,
             "dtype": DTYPE[args.graph],
-            "data": "synthetic (seeded SplitMix64 reads generated in HBM)",
+            "data": ("synthetic genomic stream (reads of a %d-base random genome, both strands, 1%% substitutions, "
+                     "generated in HBM)" % args.genome) if args.genome else
+                    "synthetic (seeded SplitMix64 reads generated in HBM)",
             "config": {
                 "workload": runner.config_name(),
                 "k": k, "n_tables": nt, "table_sizes": sizes, "reads_per_gpu": nreads,
                 "read_len": L, "kmers_per_gpu_per_step": nkmers, "bigcount": args.bigcount,
                 "batch_kmers": args.batch_kmers,
                 "parallelism": ("shard%d" % world) if world > 1 else "single",
+                "path": "get_median_count" if args.query else "consume",
+                "hash": "murmur3" if args.murmur else "twobit",
+                "genome": args.genome or None,
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
             "check": check_info,
         }
+        if world > 1:
+            line["rccl"] = runner.rccl_info()
         print(json.dumps(line), flush=True)
     runner.close()
 
@@ -290,35 +355,64 @@ class SingleGpuBench(object):
 
     def config_name(self):
         a = self.args
-        return "%s k=%d %dx%.0e, %d x %d bp synthetic reads, 1xMI355X" % (
-            a.graph, a.k, a.tables, a.x, a.reads, a.read_len)
+        what = "get_median_count over" if a.query else "consume of"
+        return "%s k=%d %dx%.0e, %s %d x %d bp synthetic %sreads, 1xMI355X" % (
+            a.graph, a.k, a.tables, a.x, what, a.reads, a.read_len, "genomic " if a.genome else "")
+
+    def _alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        self._ck(self.lib.kh_device_malloc(self.device, nbytes, ctypes.byref(p)))
+        self.bufs.append(p)
+        return p
 
     def setup(self):
         import khmer_amd
         from khmer_amd import synth
         from khmer_amd._lib import lib, check
         a = self.args
-        self.lib, self._ck = lib, check
+        self.lib, self._ck, self.bufs = lib, check, []
         self.g = getattr(khmer_amd, a.graph)(a.k, a.x, a.tables)
         if a.bigcount:
             self.g.set_use_bigcount(True)
         check(lib.kh_graph_set_batch_kmers(self.g._g, a.batch_kmers))
         self.nkmers = a.reads * (a.read_len - a.k + 1)
         nwords = a.reads * a.read_len // 32 + 2
-        self.words, self.koff = ctypes.c_void_p(), ctypes.c_void_p()
-        check(lib.kh_device_malloc(self.device, nwords * 8, ctypes.byref(self.words)))
-        check(lib.kh_device_malloc(self.device, (a.reads + 1) * 8, ctypes.byref(self.koff)))
-        check(lib.kh_synth_packed_device(self.device, synth.SEED, 0, a.reads, a.read_len, a.k,
-                                         self.words, self.koff))
+        self.words = self._alloc(nwords * 8)
+        self.koff = self._alloc((a.reads + 1) * 8)
+        ks = min(a.k, 32)   # the packed stream itself does not depend on k
+        if a.genome:
+            check(lib.kh_synth_genomic_device(self.device, synth.SEED, a.genome, 0, a.reads, a.read_len, ks,
+                                              self.words, self.koff))
+        else:
+            check(lib.kh_synth_packed_device(self.device, synth.SEED, 0, a.reads, a.read_len, ks, self.words,
+                                             self.koff))
+        self.reads = self.words
+        if a.murmur:   # Counttable family: the same bases as ASCII
+            self.reads = self._alloc(a.reads * a.read_len + 64)
+            check(lib.kh_unpack_ascii_device(self.device, self.words, a.reads * a.read_len, self.reads))
+        if a.query:
+            self.med = self._alloc(a.reads * 2 + 64)
+            self.avg = self._alloc(a.reads * 4 + 64)
+            self.sd = self._alloc(a.reads * 4 + 64)
+            self._consume()   # the tables being queried (untimed)
+
+    def _consume(self):
+        a = self.args
+        if a.murmur:
+            self._ck(self.lib.kh_consume_bytes_fixed_device(self.g._g, self.reads, a.reads, a.read_len))
+        elif a.variable_path:
+            self._ck(self.lib.kh_consume_packed_device(self.g._g, self.words, self.koff, a.reads, self.nkmers))
+        else:
+            self._ck(self.lib.kh_consume_packed_fixed_device(self.g._g, self.words, a.reads, a.read_len))
 
     def step(self):
+        a = self.args
+        if a.query:
+            self._ck(self.lib.kh_median_counts_fixed_device(self.g._g, self.reads, a.reads, a.read_len, self.med,
+                                                            self.avg, self.sd))
+            return
         self._ck(self.lib.kh_graph_clear(self.g._g))
-        if self.args.variable_path:
-            self._ck(self.lib.kh_consume_packed_device(self.g._g, self.words, self.koff,
-                                                       self.args.reads, self.nkmers))
-        else:
-            self._ck(self.lib.kh_consume_packed_fixed_device(self.g._g, self.words, self.args.reads,
-                                                             self.args.read_len))
+        self._consume()
 
     def sync(self):
         self._ck(self.lib.kh_device_synchronize(self.device))
@@ -336,13 +430,28 @@ class SingleGpuBench(object):
         return kernel_stats(self.lib, self.g._g)
 
     def check(self):
-        """Counters of the last step (the full workload into empty tables)."""
-        return {"n_unique_kmers": self.g.n_unique_kmers(), "n_occupied": self.g.n_occupied()}
+        """Counters of the last consume (the full workload into empty tables);
+        --query: also a checksum of the medians."""
+        out = {"n_unique_kmers": self.g.n_unique_kmers(), "n_occupied": self.g.n_occupied()}
+        if self.args.query:
+            import hashlib
+            n = self.args.reads
+            med = (ctypes.c_uint16 * n)()
+            self._ck(self.lib.kh_device_synchronize(self.device))
+            hip_copy_d2h(self.lib, self.device, med, self.med, n * 2)
+            out["median_sha256"] = hashlib.sha256(bytes(med)).hexdigest()
+        return out
 
     def close(self):
-        self.lib.kh_device_free(self.device, self.words)
-        self.lib.kh_device_free(self.device, self.koff)
+        for p in self.bufs:
+            self.lib.kh_device_free(self.device, p)
         del self.g
+
+
+def hip_copy_d2h(lib, device, dst, src, nbytes):
+    """device -> host copy through the library (no PyTorch on the host side)."""
+    from khmer_amd._lib import check
+    check(lib.kh_device_copy(device, dst, src, nbytes))
 
 
 if __name__ == "__main__":

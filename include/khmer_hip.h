@@ -141,6 +141,10 @@ int kh_consume_packed_device(kh_graph *g, const uint64_t *d_words, const uint64_
 /* the same for reads of one length (read_len >= k): no offset array, read r
  * starts at base r*read_len (the common fixed-length sequencing case). */
 int kh_consume_packed_fixed_device(kh_graph *g, const uint64_t *d_words, uint64_t nreads, uint32_t read_len);
+/* Murmur graphs (Counttable family, include/oxli/hashtable.hh:494-627): ASCII
+ * reads of one length already in device memory, read r at byte r*read_len;
+ * MurmurKmerHashIterator over each (src/oxli/kmer_hash.cc:177-198). */
+int kh_consume_bytes_fixed_device(kh_graph *g, const uint8_t *d_bytes, uint64_t nreads, uint32_t read_len);
 /* explicit hashes: Hashtable::count/add(HashIntoType) (include/oxli/hashtable.hh:222-243);
  * is_new[n] (nullable) receives Storage::add's return per hash, in order. */
 int kh_add_hashes(kh_graph *g, const uint64_t *hashes, uint64_t n, uint8_t *is_new);
@@ -152,6 +156,12 @@ int kh_get_counts(kh_graph *g, const uint64_t *hashes, uint64_t n, uint16_t *out
  * with no k-mer get status[r] = 1 (the reference throws for them). */
 int kh_median_counts(kh_graph *g, const char *seqs, const uint64_t *offsets, uint64_t nreads,
                      uint16_t *med, float *avg, float *stddev, uint8_t *status);
+/* get_median_count per read of device-resident fixed-length reads (2-bit
+ * packed words for 2-bit graphs, ASCII bytes for Murmur graphs), outputs in
+ * device memory; read_len - k + 1 <= 256.  Same values as kh_median_counts
+ * (src/oxli/hashtable.cc:299-328; scripts/count-median.py:123 is the caller). */
+int kh_median_counts_fixed_device(kh_graph *g, const void *d_reads, uint64_t nreads, uint32_t read_len,
+                                  uint16_t *d_med, float *d_avg, float *d_stddev);
 /* Hashtable::abundance_distribution (src/oxli/hashtable.cc:451-493);
  * dist[65536]. */
 int kh_abundance_distribution(kh_graph *g, kh_parser *p, kh_graph *tracking, uint64_t *dist);
@@ -189,7 +199,11 @@ int kh_synth_packed_device(int device, uint64_t seed, uint64_t r0, uint64_t nrea
  * strand, 1% substitutions; same packing as kh_synth_packed_device. */
 int kh_synth_genomic_device(int device, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int read_len,
                             int k, uint64_t *d_words, uint64_t *d_kmer_off);
+/* 2-bit packed bases -> ASCII bytes (A/T/C/G), both in device memory */
+int kh_unpack_ascii_device(int device, const uint64_t *d_words, uint64_t nbases, uint8_t *d_bytes);
 int kh_device_malloc(int device, uint64_t bytes, void **out);
+/* synchronous copy between host and/or device memory of `device` */
+int kh_device_copy(int device, void *dst, const void *src, uint64_t nbytes);
 int kh_device_free(int device, void *p);
 int kh_device_synchronize(int device);
 /* per-kernel HIP-event timing on the graph's stream: on=1 resets and enables;

@@ -71,6 +71,8 @@ SIGNATURES = {
     "kh_consume_seqs": (i32, [P, ctypes.c_char_p, PU64, u64, i32, PU64]),
     "kh_consume_packed_device": (i32, [P, P, P, u64, u64]),
     "kh_consume_packed_fixed_device": (i32, [P, P, u64, u32]),
+    "kh_consume_bytes_fixed_device": (i32, [P, P, u64, u32]),
+    "kh_median_counts_fixed_device": (i32, [P, P, u64, u32, P, P, P]),
     "kh_add_hashes": (i32, [P, PU64, u64, ctypes.POINTER(ctypes.c_uint8)]),
     "kh_get_counts": (i32, [P, PU64, u64, ctypes.POINTER(ctypes.c_uint16)]),
     "kh_median_counts": (i32, [P, ctypes.c_char_p, PU64, u64, ctypes.POINTER(ctypes.c_uint16),
@@ -89,7 +91,9 @@ SIGNATURES = {
     "kh_graph_load_tagset": (i32, [P, ctypes.c_char_p, i32]),
     "kh_synth_packed_device": (i32, [i32, u64, u64, u64, i32, i32, P, P]),
     "kh_synth_genomic_device": (i32, [i32, u64, u64, u64, u64, i32, i32, P, P]),
+    "kh_unpack_ascii_device": (i32, [i32, P, u64, P]),
     "kh_device_malloc": (i32, [i32, u64, ctypes.POINTER(P)]),
+    "kh_device_copy": (i32, [i32, P, P, u64]),
     "kh_device_free": (i32, [i32, P]),
     "kh_device_synchronize": (i32, [i32]),
     "kh_graph_set_profiling": (i32, [P, i32]),

@@ -413,6 +413,28 @@ int kh_consume_packed_fixed_device(kh_graph *h, const uint64_t *d_words, uint64_
     });
 }
 
+int kh_consume_bytes_fixed_device(kh_graph *h, const uint8_t *d_bytes, uint64_t nreads, uint32_t read_len) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        if (g->hash != MURMUR) fail(KH_EVALUE, "ASCII device input requires a Murmur hashing graph");
+        engine_consume_bytes_fixed(g, d_bytes, nreads, read_len);
+    });
+}
+
+int kh_median_counts_fixed_device(kh_graph *h, const void *d_reads, uint64_t nreads, uint32_t read_len,
+                                  uint16_t *d_med, float *d_avg, float *d_stddev) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        engine_median_fixed_device(g, d_reads, nreads, read_len, d_med, d_avg, d_stddev);
+    });
+}
+
 int kh_add_hashes(kh_graph *h, const uint64_t *hashes, uint64_t n, uint8_t *is_new) {
     return guard([&] {
         CHECK_PTR(h);
@@ -860,6 +882,17 @@ extern "C" int kh_synth_genomic_device(int device, uint64_t seed, uint64_t genom
         if (read_len < k || k < 1 || k > 32) fail(KH_EVALUE, "need 1 <= k <= read length and k <= 32");
         if (genome < (uint64_t)read_len) fail(KH_EVALUE, "genome shorter than a read");
         engine_synth_packed(device, seed, genome, r0, nreads, read_len, k, d_words, d_kmer_off);
+    });
+}
+
+extern "C" int kh_unpack_ascii_device(int device, const uint64_t *d_words, uint64_t nbases, uint8_t *d_bytes) {
+    return guard([&] { engine_unpack_ascii(device, d_words, nbases, d_bytes); });
+}
+
+extern "C" int kh_device_copy(int device, void *dst, const void *src, uint64_t nbytes) {
+    return guard([&] {
+        KH_HIP(hipSetDevice(device));
+        KH_HIP(hipMemcpy(dst, src, nbytes, hipMemcpyDefault));
     });
 }
 

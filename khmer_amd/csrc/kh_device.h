@@ -169,4 +169,78 @@ KH_HD uint64_t murmur_canonical(const uint8_t *s, int k) {
     return h ^ r;
 }
 
+// ---- device fast path: Murmur over byte-aligned little-endian words ----
+// k-mers of up to MURMUR_WORDS_MAX bytes are hashed from eight aligned 8-byte
+// loads per window (a funnel shift aligns them), the reverse complement from a
+// second window into the reads' precomputed reverse-complement stream
+// (k_revcomp_reads), so no byte loads and no complement table per k-mer.
+constexpr int MURMUR_WORDS_MAX = 56;
+
+KH_HD uint64_t murmur_tail_mask(int nbytes) { return nbytes >= 8 ? ~0ull : ((1ull << (8 * nbytes)) - 1); }
+
+// MurmurHash3_x64_128 h1 of `len` (<= 56) bytes held little-endian in v[0..6]
+KH_HD uint64_t murmur3_h1_words(const uint64_t *v, int len) {
+    const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+    uint64_t h1 = 0, h2 = 0;
+    const int nblocks = len / 16;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        if (i < nblocks) {
+            uint64_t k1 = v[2 * i], k2 = v[2 * i + 1];
+            k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+            h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+            k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+            h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+        }
+    }
+    const int rem = len & 15;
+    uint64_t t1 = 0, t2 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        if (i == nblocks) { t1 = v[2 * i]; t2 = i < 3 ? v[2 * i + 1] : 0; }
+    if (rem > 8) {
+        uint64_t k2 = t2 & murmur_tail_mask(rem - 8);
+        k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    }
+    if (rem > 0) {
+        uint64_t k1 = t1 & murmur_tail_mask(rem);
+        k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    }
+    h1 ^= (uint64_t)len; h2 ^= (uint64_t)len;
+    h1 += h2; h2 += h1;
+    h1 = fmix64(h1); h2 = fmix64(h2);
+    h1 += h2;
+    return h1;
+}
+
+// the 7 little-endian words of the bytes at p (8 aligned loads; reads at most
+// 7 bytes past p + 56)
+KH_HD void load_window(const uint8_t *p, uint64_t *v) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const uint64_t *w = (const uint64_t *)(uintptr_t)(a & ~7ull);
+    const unsigned sh = (unsigned)(a & 7) * 8;
+    uint64_t x[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) x[i] = w[i];
+#pragma unroll
+    for (int i = 0; i < 7; i++) v[i] = sh ? ((x[i] >> sh) | (x[i + 1] << (64 - sh))) : x[i];
+}
+
+// canonical Murmur hash of the k-mer at p whose reverse complement is at q
+// (same value as murmur_canonical(p, k) for k <= MURMUR_WORDS_MAX)
+KH_HD uint64_t murmur_canonical_windows(const uint8_t *p, const uint8_t *q, int k) {
+    uint64_t v[7], u[7];
+    load_window(p, v);
+    load_window(q, u);
+    const uint64_t h = murmur3_h1_words(v, k);
+    bool self = true;
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        const int nb = k - 8 * i;
+        if (nb > 0) self = self && ((v[i] ^ u[i]) & murmur_tail_mask(nb)) == 0;
+    }
+    if (self) return h;
+    return h ^ murmur3_h1_words(u, k);
+}
+
 }  // namespace kh

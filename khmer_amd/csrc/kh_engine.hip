@@ -959,11 +959,27 @@ static SrcTwoBit src_twobit(Graph *g, const uint64_t *d_words) {
     s.k = g->k;
     return s;
 }
-static SrcBytes src_bytes(Graph *g, const uint8_t *d_bytes) {
+// a Murmur source over nbytes of reads (k-mer offsets d_koff, or fixed kpr
+// k-mers per read when d_koff is null); builds the reads' reverse-complement
+// stream in the workspace first
+static SrcBytes src_bytes(Graph *g, const uint8_t *d_bytes, const uint64_t *d_koff, uint64_t nreads, uint64_t kpr,
+                          uint64_t nbytes) {
     SrcBytes s{};
     s.bytes = d_bytes;
     s.k = g->k;
+    Workspace &w = g->ws;
+    ensure((void **)&w.d_rbytes, &w.cap_rbytes, nbytes + 64, 1);
+    s.rbytes = w.d_rbytes;
+    if (nreads && g->k <= MURMUR_WORDS_MAX) {
+        const unsigned grid = (unsigned)std::min<uint64_t>((nreads + 3) / 4, 16384);
+        hipLaunchKernelGGL(k_revcomp_reads, dim3(grid), dim3(256), 0, g->stream, d_bytes, d_koff, kpr, g->k, nreads,
+                           w.d_rbytes);
+        KH_HIP(hipGetLastError());
+    }
     return s;
+}
+static SrcBytes src_bytes_host(Graph *g, const HostBatch &b) {
+    return src_bytes(g, g->ws.d_bytes, g->ws.d_koff, b.nreads(), 0, b.bytes.size());
 }
 
 void engine_consume_twobit(Graph *g, const uint64_t *d_words, const uint64_t *d_koff, uint64_t nreads,
@@ -980,7 +996,10 @@ void engine_consume_twobit_fixed(Graph *g, const uint64_t *d_words, uint64_t nre
 
 void engine_consume_bytes(Graph *g, const uint8_t *d_bytes, const uint64_t *d_koff, uint64_t nreads,
                           uint64_t nkmers, const PassOut *out) {
-    consume_reads(g, src_bytes(g, d_bytes), d_koff, nreads, nkmers, 0, out);
+    uint64_t kend = 0;
+    KH_HIP(hipMemcpy(&kend, d_koff + nreads, 8, hipMemcpyDeviceToHost));
+    consume_reads(g, src_bytes(g, d_bytes, d_koff, nreads, 0, kend + nreads * (uint64_t)(g->k - 1)), d_koff, nreads,
+                  nkmers, 0, out);
 }
 
 // Passes run in stream order, so per-k-mer outputs of consecutive passes are
@@ -1008,7 +1027,7 @@ static void upload_batch(Graph *g, const HostBatch &b) {
     ensure((void **)&w.d_koff, &w.cap_koff, nr + 1, 8);
     KH_HIP(hipMemcpyAsync(w.d_koff, b.koff.data(), (nr + 1) * 8, hipMemcpyHostToDevice, g->stream));
     if (b.hash == MURMUR) {
-        ensure((void **)&w.d_bytes, &w.cap_bytes, b.bytes.size() + 8, 1);
+        ensure((void **)&w.d_bytes, &w.cap_bytes, b.bytes.size() + 64, 1);
         KH_HIP(hipMemcpyAsync(w.d_bytes, b.bytes.data(), b.bytes.size(), hipMemcpyHostToDevice, g->stream));
     } else {
         const uint64_t nw = (b.nbases + 31) / 32 + 1;
@@ -1029,7 +1048,7 @@ void engine_consume_host(Graph *g, const HostBatch &b, const PassOut *out) {
     upload_batch(g, b);
     const uint64_t kpr = batch_kpr(b);
     if (b.hash == MURMUR)
-        consume_reads(g, src_bytes(g, g->ws.d_bytes), g->ws.d_koff, b.nreads(), b.nkmers(), kpr, out);
+        consume_reads(g, src_bytes_host(g, b), g->ws.d_koff, b.nreads(), b.nkmers(), kpr, out);
     else
         consume_reads(g, src_twobit(g, g->ws.d_words), g->ws.d_koff, b.nreads(), b.nkmers(), kpr, out);
 }
@@ -1043,7 +1062,7 @@ void engine_hash_batch(Graph *g, const HostBatch &b, uint64_t *h_out) {
     const uint64_t tiles = (nk + Q_TILE - 1) / Q_TILE;
     const size_t lds = 16 + (Q_TILE + 2) * 8;
     if (b.hash == MURMUR) {
-        SrcBytes s = src_bytes(g, g->ws.d_bytes);
+        SrcBytes s = src_bytes_host(g, b);
         s.koff = g->ws.d_koff;
         s.nreads = nr;
         hipLaunchKernelGGL(k_kmer_hashes<SrcBytes>, dim3((unsigned)tiles), dim3(Q_THREADS), lds, g->stream, s, nk, d);
@@ -1084,7 +1103,7 @@ uint64_t engine_consume_filtered(Graph *g, const HostBatch &b, const BandMask &f
     const uint64_t tiles = (nk + Q_TILE - 1) / Q_TILE;
     const size_t lds = 16 + (Q_TILE + 2) * 8;
     if (b.hash == MURMUR) {
-        SrcBytes s = src_bytes(g, g->ws.d_bytes);
+        SrcBytes s = src_bytes_host(g, b);
         s.koff = g->ws.d_koff;
         s.nreads = nr;
         hipLaunchKernelGGL(k_kmer_filter<SrcBytes>, dim3((unsigned)tiles), dim3(Q_THREADS), lds, g->stream, s, nk, F,
@@ -1138,7 +1157,7 @@ void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, floa
     const size_t lds = 16 + (Q_TILE + 2) * 8;
     if (tiles) {
         if (b.hash == MURMUR) {
-            SrcBytes s = src_bytes(g, g->ws.d_bytes);
+            SrcBytes s = src_bytes_host(g, b);
             s.koff = g->ws.d_koff;
             s.nreads = nr;
             hipLaunchKernelGGL(k_kmer_counts<SrcBytes>, dim3((unsigned)tiles), dim3(Q_THREADS), lds, g->stream, g->prm,
@@ -1158,6 +1177,50 @@ void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, floa
     KH_HIP(hipMemcpyAsync(avg, d_avg, nr * 4, hipMemcpyDeviceToHost, g->stream));
     KH_HIP(hipMemcpyAsync(sd, d_sd, nr * 4, hipMemcpyDeviceToHost, g->stream));
     KH_HIP(hipStreamSynchronize(g->stream));
+}
+
+// get_median_count over device-resident fixed-length reads (packed 2-bit words
+// for 2-bit graphs, ASCII bytes for Murmur ones); outputs stay on the device
+void engine_median_fixed_device(Graph *g, const void *d_reads, uint64_t nreads, uint64_t read_len, uint16_t *d_med,
+                                float *d_avg, float *d_sd) {
+    if (read_len < (uint64_t)g->k) fail(KH_EVALUE, "reads shorter than k");
+    const uint64_t kpr = read_len - g->k + 1;
+    if (kpr > 256) fail(KH_EVALUE, "device median path takes at most 256 k-mers per read");
+    if (!nreads) return;
+    engine_sync_bigcounts(g);
+    const unsigned grid = (unsigned)std::min<uint64_t>((nreads + 3) / 4, 8192);
+    if (g->hash == MURMUR) {
+        SrcBytes s = src_bytes(g, (const uint8_t *)d_reads, nullptr, nreads, kpr, nreads * read_len);
+        set_fixed(s, kpr);
+        TIMED("median", hipLaunchKernelGGL(k_median_fixed<SrcBytes>, dim3(grid), dim3(256), 0, g->stream, g->prm, s,
+                                           nreads, (uint32_t)kpr, g->d_tab, g->d_bc_keys, g->d_bc_vals, g->d_bc_n,
+                                           d_med, d_avg, d_sd));
+    } else {
+        SrcTwoBit s = src_twobit(g, (const uint64_t *)d_reads);
+        set_fixed(s, kpr);
+        TIMED("median", hipLaunchKernelGGL(k_median_fixed<SrcTwoBit>, dim3(grid), dim3(256), 0, g->stream, g->prm, s,
+                                           nreads, (uint32_t)kpr, g->d_tab, g->d_bc_keys, g->d_bc_vals, g->d_bc_n,
+                                           d_med, d_avg, d_sd));
+    }
+    KH_HIP(hipGetLastError());
+    KH_HIP(hipStreamSynchronize(g->stream));
+    engine_collect_events(g);
+}
+
+void engine_consume_bytes_fixed(Graph *g, const uint8_t *d_bytes, uint64_t nreads, uint64_t read_len) {
+    if (read_len < (uint64_t)g->k) fail(KH_EVALUE, "reads shorter than k");
+    const uint64_t kpr = read_len - g->k + 1;
+    consume_reads(g, src_bytes(g, d_bytes, nullptr, nreads, kpr, nreads * read_len), nullptr, nreads, nreads * kpr, kpr,
+                  nullptr);
+}
+
+void engine_unpack_ascii(int device, const uint64_t *d_words, uint64_t nbases, uint8_t *d_bytes) {
+    KH_HIP(hipSetDevice(device));
+    const uint64_t nw = (nbases + 31) / 32;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nw + 255) / 256, 65536));
+    hipLaunchKernelGGL(k_unpack_ascii, dim3(grid), dim3(256), 0, nullptr, d_words, nbases, d_bytes);
+    KH_HIP(hipGetLastError());
+    KH_HIP(hipDeviceSynchronize());
 }
 
 void engine_download_table(Graph *g, int i, uint8_t *dst) {
@@ -1349,7 +1412,7 @@ Graph::~Graph() {
     Workspace &w = ws;
     void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.fullf, w.newbits, w.bc, w.bcn, w.bck, w.bcv,
                     w.off1, w.ch2, w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.xseg, w.reg_base, w.reg_cur, w.bkt_base, w.bkt_cur, w.ctr, w.d_words, w.d_koff, w.d_bytes,
-                    w.q_hashes, w.q_counts, w.frec, w.fcount};
+                    w.q_hashes, w.q_counts, w.frec, w.fcount, w.d_rbytes, w.sm_flags, w.sm_hash};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (w.h_ctr) (void)hipHostFree(w.h_ctr);

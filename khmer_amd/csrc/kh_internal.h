@@ -123,7 +123,8 @@ struct Workspace {
     // staging for host-fed batches
     uint64_t *d_words = nullptr, *d_koff = nullptr;
     uint8_t *d_bytes = nullptr;
-    uint64_t cap_words = 0, cap_koff = 0, cap_bytes = 0;
+    uint8_t *d_rbytes = nullptr;     // reverse complement of every read of d_bytes (Murmur sources)
+    uint64_t cap_words = 0, cap_koff = 0, cap_bytes = 0, cap_rbytes = 0;
     // small passes (k_small_pass): per-k-mer flags and hashes
     uint8_t *sm_flags = nullptr;
     uint64_t *sm_hash = nullptr;
@@ -245,6 +246,10 @@ struct BandMask {
 };
 uint64_t engine_consume_filtered(Graph *g, const HostBatch &b, const BandMask &f);
 void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, float *sd);
+void engine_median_fixed_device(Graph *g, const void *d_reads, uint64_t nreads, uint64_t read_len, uint16_t *d_med,
+                                float *d_avg, float *d_sd);
+void engine_consume_bytes_fixed(Graph *g, const uint8_t *d_bytes, uint64_t nreads, uint64_t read_len);
+void engine_unpack_ascii(int device, const uint64_t *d_words, uint64_t nbases, uint8_t *d_bytes);
 void engine_sync_bigcounts(Graph *g);
 void engine_download_table(Graph *g, int i, uint8_t *dst);
 void engine_upload_table(Graph *g, int i, const uint8_t *src);

@@ -190,6 +190,116 @@ __global__ void k_median(const uint64_t *koff, uint64_t nreads, uint16_t *counts
     }
 }
 
+// Hashtable::get_median_count over fixed-length device reads, one wave per read
+// (kpr = k-mers per read <= 256, four per lane): the k-mer counts stay in
+// registers.  average: the partial sums are integers below 2^24 (kpr <= 256,
+// counts <= 65535), so the reference's sequential float32 sum equals the
+// exact integer sum; the squared deviations are summed in stream order by a
+// uniform loop (the same rounding sequence as the reference); median =
+// sorted[kpr / 2] by a radix select over the counts with wave ballots.
+template <class Src>
+__global__ void __launch_bounds__(256) k_median_fixed(Params P, Src src, uint64_t nreads, uint32_t kpr,
+                                                      const uint8_t *tab, const uint64_t *bc_keys,
+                                                      const uint16_t *bc_vals, uint64_t bc_n, uint16_t *med,
+                                                      float *avg, float *sd) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t r = wave; r < nreads; r += nwaves) {
+        uint32_t c[4];
+        bool ok[4];
+        uint32_t sum = 0, mx = 0;
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const uint32_t t = lane + 64u * s;
+            ok[s] = t < kpr;
+            c[s] = ok[s] ? get_count_dev(P, tab, kmer_hash_global(src, r * kpr + t), bc_keys, bc_vals, bc_n) : 0;
+            sum += c[s];
+            mx = c[s] > mx ? c[s] : mx;
+        }
+        sum = (uint32_t)wave_sum(sum);
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t y = __shfl_xor(mx, d, 64);
+            mx = y > mx ? y : mx;
+        }
+        const float n = (float)kpr;
+        const float average = div_rn_exact((float)sum, n);
+        float d2[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const float d = __fsub_rn((float)c[s], average);
+            d2[s] = __fmul_rn(d, d);
+        }
+        float var = 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const uint32_t lim = kpr > 64u * s ? min(64u, kpr - 64u * s) : 0u;
+            const int v = __float_as_int(d2[s]);
+            for (uint32_t l = 0; l < lim; l++) var = __fadd_rn(var, __int_as_float(__builtin_amdgcn_readlane(v, l)));
+        }
+        var = sqrt_rn_exact(div_rn_exact(var, n));
+        // radix select of element kpr / 2
+        uint32_t m = kpr / 2, prefix = 0;
+        const int nbits = 32 - __clz(mx | 1);
+        for (int b = nbits - 1; b >= 0; b--) {
+            uint32_t cnt0 = 0;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const bool cand = ok[s] && ((c[s] >> b) >> 1) == ((prefix >> b) >> 1) && !((c[s] >> b) & 1);
+                cnt0 += __popcll(__ballot(cand));
+            }
+            if (m >= cnt0) {
+                m -= cnt0;
+                prefix |= 1u << b;
+            }
+        }
+        if (lane == 0) {
+            med[r] = (uint16_t)prefix;
+            avg[r] = average;
+            sd[r] = var;
+        }
+    }
+}
+
+// every read of a byte batch reverse-complemented in place (the complement of
+// _revcomp, src/oxli/kmer_hash.cc:52-55, IUPAC and all): read r occupies bytes
+// [koff[r] + r*(k-1), +len) (fixed length: [r*L, +L)); one wave per read
+__global__ void k_revcomp_reads(const uint8_t *bytes, const uint64_t *koff, uint64_t kpr, int k, uint64_t nreads,
+                                uint8_t *rbytes) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t r = wave; r < nreads; r += nwaves) {
+        uint64_t start, len;
+        if (koff) {
+            start = koff[r] + r * (uint64_t)(k - 1);
+            len = koff[r + 1] - koff[r] + (uint64_t)(k - 1);
+        } else {
+            len = kpr + (uint64_t)(k - 1);
+            start = r * len;
+        }
+        for (uint64_t t = lane; t < len; t += 64) rbytes[start + t] = (uint8_t)iupac_comp(bytes[start + len - 1 - t]);
+    }
+}
+
+// 2-bit packed bases -> ASCII (code 0..3 = A, T, C, G; kh_device.h order)
+__global__ void k_unpack_ascii(const uint64_t *words, uint64_t nbases, uint8_t *out) {
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w * 32 < nbases;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t x = words[w];
+        uint8_t b[32];
+#pragma unroll
+        for (int i = 0; i < 32; i++) b[i] = "ATCG"[(x >> (62 - 2 * i)) & 3];
+        if (w * 32 + 32 <= nbases) {
+            uint4 *o = (uint4 *)(out + w * 32);
+            o[0] = *(const uint4 *)&b[0];
+            o[1] = *(const uint4 *)&b[16];
+        } else {
+            for (uint64_t i = 0; w * 32 + i < nbases; i++) out[w * 32 + i] = b[i];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // batch boundaries of a device read set: chunk i starts at the last read whose
 // k-mer offset is <= koff[0] + i*B

@@ -58,11 +58,24 @@ struct SrcTwoBit : SrcCommon {
     }
 };
 
+// ASCII reads for the Murmur (Counttable family) hash.  rbytes holds every
+// read reverse-complemented in place (k_revcomp_reads): the reverse complement
+// of the k-mer at read position i is the window at position len - k - i
 struct SrcBytes : SrcCommon {
     const uint8_t *bytes;
+    const uint8_t *rbytes;
     static constexpr bool kReads = true;
     __device__ __forceinline__ uint64_t at(uint64_t ja, uint64_t r) const {
-        return murmur_canonical(bytes + ja + r * (uint64_t)(k - 1), k);
+        const uint64_t pos = ja + r * (uint64_t)(k - 1);
+        if (k > MURMUR_WORDS_MAX) return murmur_canonical(bytes + pos, k);
+        uint64_t rpos;
+        if (kpr) {
+            rpos = r * (kpr + (uint64_t)(k - 1)) + (kpr - 1) - (ja - r * kpr);
+        } else {
+            const uint64_t k0 = koff[r - rbase], nk = koff[r - rbase + 1] - k0;
+            rpos = k0 + r * (uint64_t)(k - 1) + (nk - 1) - (ja - k0);
+        }
+        return murmur_canonical_windows(bytes + pos, rbytes + rpos, k);
     }
     using Pend = uint64_t;   // Murmur reads k bytes: hashed at fetch time
     __device__ __forceinline__ Pend fetch(uint64_t ja, uint64_t r) const { return at(ja, r); }

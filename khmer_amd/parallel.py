@@ -267,8 +267,9 @@ class ShardedCountgraphBench(object):
 
     def config_name(self):
         a = self.args
-        return a.graph + " k=%d %dx%.0e sharded over %dxMI355X, %d x %d bp synthetic reads per GPU" % (
-            a.k, a.tables, a.x, self.world, a.reads, a.read_len)
+        return a.graph + " k=%d %dx%.0e sharded over %dxMI355X, %d x %d bp synthetic %sreads per GPU%s" % (
+            a.k, a.tables, a.x, self.world, a.reads, a.read_len, "genomic " if a.genome else "",
+            " (strong scaling: %d reads in all)" % (a.reads * self.world) if a.strong else "")
 
     def setup(self):
         from . import synth
@@ -288,8 +289,12 @@ class ShardedCountgraphBench(object):
         check(lib.kh_device_malloc(self.device, nwords * 8, ctypes.byref(self.words)))
         check(lib.kh_device_malloc(self.device, (a.reads + 1) * 8, ctypes.byref(self.koff)))
         # every rank's own reads: the rank-th block of the synthetic stream
-        check(lib.kh_synth_packed_device(self.device, synth.SEED, self.rank * a.reads, a.reads, a.read_len, a.k,
-                                         self.words, self.koff))
+        if a.genome:
+            check(lib.kh_synth_genomic_device(self.device, synth.SEED, a.genome, self.rank * a.reads, a.reads,
+                                              a.read_len, a.k, self.words, self.koff))
+        else:
+            check(lib.kh_synth_packed_device(self.device, synth.SEED, self.rank * a.reads, a.reads, a.read_len, a.k,
+                                             self.words, self.koff))
 
     def step(self):
         self.g.clear()
