@@ -12,7 +12,11 @@
 #include <fstream>
 #include <memory>
 #include <new>
+#include <condition_variable>
+#include <deque>
+#include <exception>
 #include <string>
+#include <thread>
 
 #include "../../include/khmer_hip.h"
 #include "kh_internal.h"
@@ -26,6 +30,8 @@ uint64_t parser_num_reads(Parser *p);
 bool parser_is_complete(Parser *p);
 void parser_fill_batch(Parser *p, HostBatch &b, int k, uint64_t max_kmers, uint64_t max_bases, bool *done,
                        uint64_t *taken);
+void parser_fill_raw(Parser *p, RawBatch &b, int k, uint64_t max_kmers, uint64_t max_bases, bool *done,
+                     uint64_t *taken);
 void engine_hash_batch(Graph *g, const HostBatch &b, uint64_t *h_out);
 void engine_synth_packed(int device, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L, int k,
                          uint64_t *d_words, uint64_t *d_koff);
@@ -279,6 +285,136 @@ static void consume_batch(Graph *g, const HostBatch &b, int mode, uint64_t *cons
 
 static uint64_t batch_bases_cap(Graph *g) { return g->batch_kmers * 2 + (1u << 20); }
 
+// Host threads for the pipelined feed: OMP_NUM_THREADS (the job's CPU share
+// on a shared node) or the hardware threads, at most 16.
+static int feed_threads() {
+    int n = (int)std::thread::hardware_concurrency();
+    const char *e = getenv("OMP_NUM_THREADS");
+    if (e && atoi(e) > 0) n = std::min(n > 0 ? n : 1, atoi(e));
+    const char *f = getenv("KH_FEED_THREADS");   // development override
+    if (f && atoi(f) > 0) n = atoi(f);
+    return std::max(1, std::min(16, n));
+}
+
+// consume_seqfile (mode 0) as a pipeline: one reader thread runs the parser
+// (FastxReader::get_next_read semantics, read_parsers.cc:329-372) into raw
+// batches; packer threads clean and 2-bit pack them (_to_valid_dna,
+// read_parsers.cc:53-69); the calling thread uploads and consumes them on the
+// device in parse order, so tables and counters equal the serial path's.  A
+// parse error stops the reader: every read before it is consumed, then the
+// error is raised (as the reference does).
+struct FeedSlot {
+    RawBatch raw;
+    HostBatch packed;
+    bool ready = false;
+};
+static void consume_pipelined(Graph *g, Parser *parser, uint64_t *nreads_out, uint64_t *consumed) {
+    const int T = feed_threads();
+    const int npack = std::max(1, T - 1);
+    const int depth = npack + 2;                       // batches in flight
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::unique_ptr<FeedSlot>> slots;       // parse order
+    uint64_t seq_parsed = 0;                           // batches the reader produced
+    bool reader_done = false, stop = false;
+    std::exception_ptr reader_err;
+    uint64_t taken = 0;
+    std::deque<FeedSlot *> to_pack;
+    // feed batches of at most 2^27 k-mers: host memory stays ~0.2 GB per batch in flight
+    const uint64_t maxk = std::min<uint64_t>(g->batch_kmers, 1ull << 27), maxb = maxk * 2 + (1u << 20);
+    const int k = g->k, hash = g->hash;
+    std::thread reader([&] {
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || (int)slots.size() < depth; });
+                if (stop) break;
+            }
+            std::unique_ptr<FeedSlot> sl(new FeedSlot());
+            bool done = false;
+            uint64_t t = 0;
+            std::exception_ptr err;
+            try {
+                parser_fill_raw(parser, sl->raw, k, maxk, maxb, &done, &t);
+            } catch (...) {
+                err = std::current_exception();
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            taken += t;
+            to_pack.push_back(sl.get());
+            slots.push_back(std::move(sl));
+            seq_parsed++;
+            if (err) reader_err = err;
+            if (err || done) reader_done = true;
+            cv.notify_all();
+            if (reader_done) break;
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        reader_done = true;
+        cv.notify_all();
+    });
+    std::vector<std::thread> packers;
+    for (int i = 0; i < npack; i++)
+        packers.emplace_back([&] {
+            for (;;) {
+                FeedSlot *sl;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return stop || !to_pack.empty() || reader_done; });
+                    if (to_pack.empty()) {
+                        if (stop || reader_done) return;
+                        continue;
+                    }
+                    sl = to_pack.front();
+                    to_pack.pop_front();
+                }
+                HostBatch &b = sl->packed;
+                b.hash = hash;
+                const char *p = sl->raw.seq.data();
+                for (uint32_t n : sl->raw.len) {
+                    b.append(p, n, k, true);
+                    p += n;
+                }
+                std::vector<char>().swap(sl->raw.seq);
+                std::lock_guard<std::mutex> lk(mu);
+                sl->ready = true;
+                cv.notify_all();
+            }
+        });
+    auto finish = [&] {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+            cv.notify_all();
+        }
+        reader.join();
+        for (auto &t : packers) t.join();
+    };
+    try {
+        for (;;) {
+            std::unique_ptr<FeedSlot> sl;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return (!slots.empty() && slots.front()->ready) || (reader_done && slots.empty()); });
+                if (slots.empty()) break;
+                sl = std::move(slots.front());
+                slots.pop_front();
+                cv.notify_all();
+            }
+            if (sl->packed.nkmers()) {
+                engine_consume_host(g, sl->packed, nullptr);
+                *consumed += sl->packed.nkmers();
+            }
+        }
+    } catch (...) {
+        finish();
+        throw;
+    }
+    finish();
+    *nreads_out = taken;
+    if (reader_err) std::rethrow_exception(reader_err);
+}
+
 extern "C" {
 
 int kh_consume_parser(kh_graph *h, kh_parser *ph, int mode, uint32_t *reads, uint64_t *kmers) {
@@ -290,10 +426,22 @@ int kh_consume_parser(kh_graph *h, kh_parser *ph, int mode, uint32_t *reads, uin
         Graph *g = h->g;
         std::lock_guard<std::recursive_mutex> lk(g->mu);
         KH_HIP(hipSetDevice(g->device));
+        uint64_t consumed = 0, nreads = 0;
+        if (mode == 0 && feed_threads() > 1) {
+            try {
+                consume_pipelined(g, ph->p, &nreads, &consumed);
+            } catch (...) {
+                *reads = (uint32_t)nreads;
+                *kmers = consumed;
+                throw;
+            }
+            *reads = (uint32_t)nreads;
+            *kmers = consumed;
+            return;
+        }
         HostBatch b;
         b.hash = g->hash;
         bool done = false;
-        uint64_t consumed = 0, nreads = 0;
         while (!done) {
             b.clear();
             try {

@@ -200,6 +200,13 @@ struct HostBatch {
     void append(const char *s, size_t len, int k, bool clean);
 };
 
+// raw reads for the pipelined host feed: concatenated sequences >= k bases
+struct RawBatch {
+    std::vector<char> seq;
+    std::vector<uint32_t> len;
+    uint64_t nkmers = 0, nreads_parsed = 0;
+};
+
 // ---- parser (kh_parser.cpp) ----
 struct Parser;
 struct ReadView {

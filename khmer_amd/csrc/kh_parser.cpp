@@ -157,6 +157,17 @@ std::unique_ptr<Source> open_source(const char *path) {
 }
 }  // namespace
 
+// isspace() of the C locale as a table (space, \t, \n, \v, \f, \r)
+static const unsigned char *ws_tab() {
+    static const struct T {
+        unsigned char t[256];
+        T() {
+            for (int c = 0; c < 256; c++) t[c] = isspace(c) ? 1 : 0;
+        }
+    } tab;
+    return tab.t;
+}
+
 struct Parser {
     std::unique_ptr<Source> src;
     std::string path;
@@ -225,7 +236,7 @@ struct Parser {
             if (after_eol && c == stop) break;
             // fast path: copy a run of sequence characters
             unsigned char *s = buf.data() + pos, *e = buf.data() + len, *q = s;
-            while (q < e && *q != '\n' && *q != '\r' && !isspace(*q)) q++;
+            while (q < e && !ws_tab()[*q]) q++;
             if (q == s) { pos++; after_eol = false; continue; }  // isolated space
             seq.append((const char *)s, (size_t)(q - s));
             pos += (size_t)(q - s);
@@ -239,10 +250,18 @@ struct Parser {
         read_line(tmp);
         if (!tmp.empty() && tmp != name) return false;
         if (at_end()) return true;
-        int c;
-        while (qual.size() < seq.size() && (c = peek()) >= 0) {
-            if (!isspace(c)) qual.push_back((char)c);
-            pos++;
+        // qualities: runs of non-space characters copied in bulk, whitespace
+        // (line breaks of multi-line records) skipped, until len(seq) are read
+        while (qual.size() < seq.size()) {
+            if (pos >= len && peek() < 0) break;
+            unsigned char *s = buf.data() + pos, *e = buf.data() + len;
+            const size_t need = seq.size() - qual.size();
+            unsigned char *lim = (size_t)(e - s) > need ? s + need : e;
+            unsigned char *q = s;
+            while (q < lim && !ws_tab()[*q]) q++;
+            if (q == s) { pos++; continue; }   // a whitespace character
+            qual.append((const char *)s, (size_t)(q - s));
+            pos += (size_t)(q - s);
         }
         if (qual.size() == seq.size()) skip_line();
         return true;
@@ -323,6 +342,26 @@ void parser_fill_batch(Parser *p, HostBatch &b, int k, uint64_t max_kmers, uint6
         if (rc == KH_END) { *done = true; break; }
         (*taken)++;
         if (p->seq.size() >= (size_t)k) b.append(p->seq.data(), p->seq.size(), k, true);
+    }
+}
+
+// Raw reads (uncleaned sequence bytes) of up to max_kmers k-mers for the
+// pipelined feed (kh_consume_parser): the same record semantics as
+// parser_fill_batch; cleaning and packing happen on the packer threads.
+void parser_fill_raw(Parser *p, RawBatch &b, int k, uint64_t max_kmers, uint64_t max_bases, bool *done,
+                     uint64_t *taken) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    *done = false;
+    while (b.nkmers < max_kmers && b.seq.size() < max_bases) {
+        int rc = p->next_read_locked();  // may throw
+        if (rc == KH_END) { *done = true; break; }
+        (*taken)++;
+        b.nreads_parsed++;
+        const size_t n = p->seq.size();
+        if (n < (size_t)k) continue;
+        b.seq.insert(b.seq.end(), p->seq.begin(), p->seq.end());
+        b.len.push_back((uint32_t)n);
+        b.nkmers += n - (size_t)k + 1;
     }
 }
 

@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""End-to-end (host-fed) rate of the drop-in path: Countgraph.consume_seqfile
+on a synthetic FASTQ in the page cache -- parse, clean, 2-bit pack, upload and
+count (src/oxli/hashtable.cc:125-150 via scripts/load-into-counting.py:143-158).
+Not the headline metric (bench.py's value is device-resident input); this is
+the PCIe/host-inclusive rate DESIGN.md reports beside it.
+
+Prints one JSON line.  The FASTQ is the benchmark's synthetic stream
+(khmer_amd/synth.py), written once with fixed-width names, then read once
+untimed so it sits in the page cache.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def write_fastq(path, nreads, L, chunk=1_000_000):
+    from khmer_amd import synth
+    width = len(str(nreads))
+    rec = 1 + 1 + width + 1 + L + 3 + L + 1     # "@r<idx>\n" seq "\n+\n" qual "\n"
+    with open(path, "wb") as fh:
+        for r0 in range(0, nreads, chunk):
+            n = min(chunk, nreads - r0)
+            out = np.empty((n, rec), dtype=np.uint8)
+            names = np.char.zfill(np.arange(r0, r0 + n).astype("U%d" % width), width).astype("S%d" % width)
+            out[:, 0] = ord("@")
+            out[:, 1] = ord("r")
+            out[:, 2:2 + width] = np.frombuffer(names.tobytes(), dtype=np.uint8).reshape(n, width)
+            out[:, 2 + width] = ord("\n")
+            o = 3 + width
+            out[:, o:o + L] = synth.read_ascii(r0, n, L)
+            out[:, o + L:o + L + 3] = np.frombuffer(b"\n+\n", dtype=np.uint8)
+            out[:, o + L + 3:o + 2 * L + 3] = ord("I")
+            out[:, o + 2 * L + 3] = ord("\n")
+            fh.write(out.tobytes())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=10_000_000)
+    ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("-k", type=int, default=21)
+    ap.add_argument("-x", type=float, default=1e9)
+    ap.add_argument("--tables", type=int, default=4)
+    ap.add_argument("--cpu-reads", type=int, default=300_000)
+    ap.add_argument("--dir", default=None, help="where to write the FASTQ (default: a temporary directory)")
+    a = ap.parse_args()
+    import khmer_amd
+    from khmer_amd import _lib
+    _lib.set_default_device(int(os.environ.get("LOCAL_RANK", "0")))
+    with tempfile.TemporaryDirectory(dir=a.dir) as tmp:
+        fq = os.path.join(tmp, "reads.fq")
+        t0 = time.perf_counter()
+        write_fastq(fq, a.reads, a.read_len)
+        t_write = time.perf_counter() - t0
+        size = os.path.getsize(fq)
+        with open(fq, "rb") as fh:
+            while fh.read(1 << 26):
+                pass
+        cg = khmer_amd.Countgraph(a.k, a.x, a.tables)
+        cg.set_use_bigcount(True)
+        # warm-up: the device pipeline's first use (workspace, code objects)
+        cg.consume("A" * (a.k + 10))
+        cg = khmer_amd.Countgraph(a.k, a.x, a.tables)
+        cg.set_use_bigcount(True)
+        t0 = time.perf_counter()
+        nr, nk = cg.consume_seqfile(fq)
+        dt = time.perf_counter() - t0
+        assert nr == a.reads and nk == a.reads * (a.read_len - a.k + 1), (nr, nk)
+        cpu = None
+        if a.cpu_reads:
+            from oracle import oracle as O
+            sub = os.path.join(tmp, "sample.fq")
+            write_fastq(sub, a.cpu_reads, a.read_len)
+            with open(sub, "rb") as fh:
+                while fh.read(1 << 26):
+                    pass
+            t = O.Table(O.BYTE, a.k, cg.hashsizes())
+            t.set_use_bigcount(True)
+            t0 = time.perf_counter()
+            _, ck = t.consume_fastx(sub)
+            cpu = {"value": ck / (time.perf_counter() - t0), "unit": "k-mers/s", "cores": 1, "kind": "port",
+                   "sample": "%d reads of the same FASTQ layout, oracle/khmer_oracle.c consume_fastx "
+                             "(parse + clean + count), 1 thread" % a.cpu_reads}
+    feed = int(os.environ.get("KH_FEED_THREADS", "0")) or None
+    print(json.dumps({
+        "metric": "k-mers/sec consume_seqfile end to end (page-cached FASTQ -> parse -> pack -> H2D -> count) "
+                  "into Countgraph (k=%d, %dx%.0e)" % (a.k, a.tables, a.x),
+        "value": nk / dt, "unit": "k-mers/s", "reads": nr, "kmers": nk, "seconds": dt,
+        "fastq_bytes": size, "fastq_GBps": size / dt / 1e9, "write_s": t_write,
+        "host_threads": os.environ.get("OMP_NUM_THREADS"), "feed_threads_override": feed,
+        "n_unique_kmers": cg.n_unique_kmers(), "n_occupied": cg.n_occupied(),
+        "cpu_baseline": cpu,
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()
