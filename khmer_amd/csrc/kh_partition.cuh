@@ -899,6 +899,8 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
     uint64_t *tail = nbase + F2;                    // [F2*SEG] pending partial segments
     uint32_t *cnt = (uint32_t *)(tail + F2 * SEG);  // [F2] records appended by this workgroup
     uint32_t *hist = cnt + F2;                      // [F2] this tile's records
+    uint32_t *s_nfl = hist + F2;                    // [1] entries of flist (F2 <= THREADS)
+    uint16_t *flist = (uint16_t *)(s_nfl + 4);      // [F2] regions whose pending tail completes this tile
     const uint32_t b = blockIdx.x / parts, p = blockIdx.x % parts;
     const uint64_t b0 = bstart[b], b1 = bend[b];
     const uint64_t len = (b1 - b0 + parts - 1) / parts;
@@ -910,6 +912,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
         cnt[d] = 0;
         hist[d] = 0;
     }
+    if (threadIdx.x == 0) *s_nfl = 0;
     // output slot of this workgroup's record number L of region d (this tile)
     auto phys = [&](uint32_t d, uint32_t L) -> uint64_t {
         const uint32_t split = (cnt[d] + BLK - 1) & ~(BLK - 1);
@@ -943,35 +946,51 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
             }
         }
         block_sync();
-        // blocks for this tile: one reservation per region that needs any
-        for (uint32_t d = threadIdx.x; d < F2; d += THREADS) {
-            const uint32_t h = hist[d], c0 = cnt[d];
-            uint64_t nb = 0;
-            if (h) {
-                const uint32_t need = ((c0 + h + BLK - 1) >> blk_sh) - ((c0 + BLK - 1) >> blk_sh);
-                if (bcur[d] == L2F_DEAD) {
-                    nb = L2F_DEAD;
-                } else if (need) {
-                    nb = atomicAdd(&reg_cur[gb + d], (unsigned long long)need * BLK);
-                    if (nb + (uint64_t)need * BLK > reg_base[gb + d + 1]) {
-                        atomicOr((unsigned long long *)&ctr[CTR_ERR], 4ull);
+        // blocks for this tile (one reservation per region that needs any) and
+        // the list of regions whose pending tail segment completes in this
+        // tile (every pending one on the last tile); F2 <= THREADS: thread d
+        // owns region d
+        {
+            const uint32_t d = threadIdx.x;
+            bool fl = false;
+            if (d < F2) {
+                const uint32_t h = hist[d], c0 = cnt[d];
+                uint64_t nb = 0;
+                const bool dead = bcur[d] == L2F_DEAD;
+                if (h) {
+                    const uint32_t need = ((c0 + h + BLK - 1) >> blk_sh) - ((c0 + BLK - 1) >> blk_sh);
+                    if (dead) {
                         nb = L2F_DEAD;
+                    } else if (need) {
+                        nb = atomicAdd(&reg_cur[gb + d], (unsigned long long)need * BLK);
+                        if (nb + (uint64_t)need * BLK > reg_base[gb + d + 1]) {
+                            atomicOr((unsigned long long *)&ctr[CTR_ERR], 4ull);
+                            nb = L2F_DEAD;
+                        }
                     }
                 }
+                nbase[d] = nb;
+                const uint32_t a = c0 & ~(SEG - 1), e = c0 + h;
+                fl = !dead && c0 != a && (last ? e : (e & ~(SEG - 1))) > a;
             }
-            nbase[d] = nb;
+            const uint64_t m = __ballot(fl);
+            if (m) {
+                uint32_t base = 0;
+                if ((threadIdx.x & 63) == 0) base = atomicAdd(s_nfl, (uint32_t)__popcll(m));
+                base = __shfl(base, 0, 64);
+                if (fl) flist[base + (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63)) - 1))] = (uint16_t)d;
+            }
         }
         block_sync();
-        // pending tails whose segment completes in this tile (all of them on the last tile)
-#pragma unroll 4
-        for (uint32_t y = threadIdx.x; y < F2 * SEG; y += THREADS) {
-            const uint32_t d = y / SEG, sl = y % SEG;
-            const uint32_t c0 = cnt[d], a = c0 & ~(SEG - 1);
-            if (c0 == a || sl >= c0 - a) continue;
-            const uint32_t e = c0 + hist[d];
-            if ((last ? e : (e & ~(SEG - 1))) <= a) continue;
-            const uint64_t pos = phys(d, a + sl);
-            if (pos != L2F_DEAD) rec_out[pos] = tail[y];
+        // flush the listed tails: 16 consecutive lanes per 128-B segment (its
+        // slots [a, c0) are this workgroup's, inside its current block)
+        {
+            const uint32_t nfl = *s_nfl;
+            for (uint32_t y = threadIdx.x; y < nfl * SEG; y += THREADS) {
+                const uint32_t d = flist[y / SEG], sl = y % SEG;
+                const uint32_t c0 = cnt[d], a = c0 & ~(SEG - 1);
+                if (a + sl < c0) rec_out[bcur[d] + ((a + sl) & (BLK - 1))] = tail[d * SEG + sl];
+            }
         }
         block_sync();   // the flushed tail slots are refilled below
 #pragma unroll
@@ -989,6 +1008,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
             }
         }
         block_sync();
+        if (threadIdx.x == 0) *s_nfl = 0;
         for (uint32_t d = threadIdx.x; d < F2; d += THREADS) {
             const uint32_t h = hist[d];
             if (!h) continue;
