@@ -269,7 +269,8 @@ static int l1f_rpt() { static const int v = env_seg("KH_L1F_RPT", L1_MAX_RPT) ==
 static size_t lds_scatter_l1f(const Params &P, bool window, int tile_kmers) {
     const size_t F1a = (P.F1 + 3) & ~3u;
     const size_t tile = (size_t)L1_THREADS * l1f_rpt();
-    return F1a * 8 * 5 + tile * 4 + F1a * 4 * 5 + tile * 2 * 2 + 64 + lds_window(window, tile_kmers);
+    return F1a * 8 * 5 + tile * 4 + F1a * 4 * 5 + tile * 2 * 2 + 64 + lds_window(window, tile_kmers) +
+           2 * L1F_TW * 8;
 }
 // as many workgroups per CU as the LDS allows, up to the kernel's register
 // budget (3 at 8 records per thread, 2 at 16); KH_L1F_WPC overrides (development)
@@ -287,8 +288,30 @@ static uint32_t l1f_workgroups(const Graph *g, uint64_t nkmers) {
 template <class Src>
 using L1FFn = void (*)(Params, Src, uint64_t, uint64_t, int, int, const uint64_t *, unsigned long long *, uint64_t *,
                        uint64_t *, int);
+// fixed-length 2-bit reads whose tiles span at most L1F_TW packed words take
+// the LDS-staged variant (k_scatter_l1f<..., TW = true>)
 template <class Src>
-static L1FFn<Src> l1f_kernel(int kpt, int rpt) {
+static bool l1f_tw(const Src &src, int kpt) {
+    if constexpr (!std::is_same<Src, SrcTwoBit>::value) return false;
+    else {
+        static const bool off = env_seg("KH_L1F_TW", 1) == 0;   // development
+        if (off || !src.kpr) return false;
+        const uint64_t T = (uint64_t)L1_THREADS * kpt;
+        const uint64_t reads = (T + src.kpr - 1) / src.kpr + 1;
+        const uint64_t span = T + reads * (uint64_t)(src.k - 1) + (uint64_t)src.k;
+        return span / 32 + 3 <= (uint64_t)L1F_TW;
+    }
+}
+template <class Src>
+static L1FFn<Src> l1f_kernel(int kpt, int rpt, bool tw = false) {
+    if (tw && rpt == 8) {
+        switch (kpt) {
+            case 1: return k_scatter_l1f<Src, 1, 8, true>;
+            case 2: return k_scatter_l1f<Src, 2, 8, true>;
+            case 4: return k_scatter_l1f<Src, 4, 8, true>;
+            default: return k_scatter_l1f<Src, 8, 8, true>;
+        }
+    }
     if (rpt == 16) {
         switch (kpt) {
             case 1: return k_scatter_l1f<Src, 1, 16>;
@@ -660,7 +683,8 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                 while (kpt * 2 * nt <= rpt) kpt *= 2;
                 const uint64_t tk = (uint64_t)L1_THREADS * kpt;
                 const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
-                TIMED("scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt), dim3(nwg), dim3(L1_THREADS),
+                TIMED("scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt, !window && l1f_tw(src, kpt)),
+                                                       dim3(nwg), dim3(L1_THREADS),
                                                        lds_scatter_l1f(P, window, (int)tk), st, P, src, nkmers, kpw,
                                                        t0, nt, w.bkt_base, (unsigned long long *)w.bkt_cur, w.rec1,
                                                        w.ctr, l1f_blk_sh()));
@@ -1328,6 +1352,7 @@ static void set_lds_limits() {
     for (int kpt : {1, 2, 4, 8, 16})
         for (int rpt : {8, 16}) {
             KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt, rpt));
+            KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt, rpt, true));
             KH_LDS_MAX(l1f_kernel<SrcBytes>(kpt, rpt));
             KH_LDS_MAX(l1f_kernel<SrcHashes>(kpt, rpt));
         }

@@ -443,7 +443,17 @@ constexpr int L1F_BLK_SH = 8;   // default block: 256 records (KH_L1F_BLK_SH)
 #define L1F_WAVES_PER_EU 6
 #endif
 
-template <class Src, int KPT, int RPT_ = L1_MAX_RPT>
+// LDS words per staged tile (TW) and where they live: after the kernel's
+// other arrays (lds_scatter_l1f adds 2 * L1F_TW words)
+constexpr int L1F_TW = 128;
+__host__ __device__ constexpr size_t l1f_tw_offset(size_t F1a, int rpt) {
+    // u64 index: 5 F1a u64 arrays, then (stage u32 + sb u16 + sj u16) per
+    // record, 5 F1a u32 arrays, s_wtot, s_meta, s_koff (the window, unused
+    // for fixed-length reads) rounded to 8 bytes
+    return (F1a * 8 * 5 + (size_t)L1_THREADS * rpt * 8 + F1a * 4 * 5 + 64 + 16 + 7) / 8;
+}
+
+template <class Src, int KPT, int RPT_ = L1_MAX_RPT, bool TW_ = false>
 __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) k_scatter_l1f(Params P, Src src, uint64_t nkmers, uint64_t kpw, int t0,
                                                            int nt, const uint64_t *bkt_base,
                                                            unsigned long long *bkt_cur, uint64_t *rec,
@@ -472,6 +482,13 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
     uint32_t *s_wtot = (uint32_t *)(sj + TILE_RECS);    // [16]
     uint64_t *s_meta = (uint64_t *)(s_wtot + 16);
     uint64_t *s_koff = s_meta + 2;
+    // TW: fixed-length 2-bit reads whose tile spans <= L1F_TW words: the
+    // tile's packed words are staged in LDS (double-buffered; the next tile's
+    // words are loaded one tile ahead, one word per thread) and every k-mer
+    // window is read from there -- no per-k-mer global loads, no prefetch
+    // registers
+    constexpr bool TW = TW_ && std::is_same<Src, SrcTwoBit>::value;
+    uint64_t *s_tw = (uint64_t *)smem + l1f_tw_offset(F1a, RPT);   // [2][L1F_TW]
     const int shift = P.s0 + P.s2;
     const uint64_t omask = (1ull << shift) - 1;
     for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) {
@@ -482,12 +499,27 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
     const uint64_t c0 = min(nkmers, (uint64_t)blockIdx.x * kpw);
     const uint64_t c1 = min(nkmers, c0 + kpw);
     const bool pre = !needs_window(src);
-    typename Src::Pend pend[KPT];
-    if (pre) {
+    constexpr int NPEND = TW ? 1 : KPT;
+    typename Src::Pend pend[NPEND];
+    if (!TW && pre) {
 #pragma unroll
-        for (int a = 0; a < KPT; a++) {
+        for (int a = 0; a < NPEND; a++) {
             const uint64_t j = c0 + (uint64_t)a * L1_THREADS + threadIdx.x;
             if (j < min(c1, c0 + TILE_KMERS)) pend[a] = kmer_fetch(src, j);
+        }
+    }
+    // first word of tile [j0, ..) (TW)
+    auto tile_w0 = [&](uint64_t j0) -> uint64_t {
+        const uint64_t ja = j0 + src.kbase;
+        return ((ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2) >> 6;
+    };
+    // words [tile_w0(j0), tile_w0(j1 - 1) + 1] hold every window of tile [j0, j1)
+    auto tile_nw = [&](uint64_t j0, uint64_t j1) -> uint32_t { return (uint32_t)(tile_w0(j1 - 1) + 2 - tile_w0(j0)); };
+    uint64_t tw_next = 0;
+    if constexpr (TW) {
+        if (c1 > c0) {
+            const uint64_t e = min(c1, c0 + TILE_KMERS);
+            if (threadIdx.x < tile_nw(c0, e)) s_tw[threadIdx.x] = src.words[tile_w0(c0) + threadIdx.x];
         }
     }
     const uint32_t ntiles = uniform_u32((uint32_t)((c1 - c0 + TILE_KMERS - 1) / TILE_KMERS));
@@ -497,6 +529,14 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
         const bool last = ti + 1 == ntiles;
         block_sync();
         TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
+        const uint64_t *tw_cur = s_tw + (ti & 1) * L1F_TW;
+        const uint64_t tw_w0 = TW ? tile_w0(j0) : 0;
+        if constexpr (TW) {   // the next tile's words, stored at the end of this tile
+            if (!last) {
+                const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
+                if (threadIdx.x < tile_nw(n0, n1)) tw_next = src.words[tile_w0(n0) + threadIdx.x];
+            }
+        }
         // per record slot q (k-mer a = q / nt of this thread): bin offset
         // inside its bucket (~0: none) and (a << 23 | bucket << 13 | tile
         // rank); the k-mer index is j0 + a * L1_THREADS + thread: 2 VGPRs per record
@@ -507,7 +547,18 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
 #pragma unroll
         for (int a = 0; a < KPT; a++) {
             const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
-            hh[a] = j < j1 ? (pre ? src.finish(pend[a]) : kmer_hash(src, s_koff, tr, j)) : 0;
+            if constexpr (TW) {
+                uint64_t h = 0;
+                if (j < j1) {
+                    const uint64_t ja = j + src.kbase;
+                    const uint64_t bpos = (ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2;
+                    const uint32_t wi = (uint32_t)((bpos >> 6) - tw_w0);
+                    h = src.finish(SrcTwoBit::Pend{tw_cur[wi], tw_cur[wi + 1], (uint32_t)(bpos & 63)});
+                }
+                hh[a] = h;
+            } else {
+                hh[a] = j < j1 ? (pre ? src.finish(pend[a]) : kmer_hash(src, s_koff, tr, j)) : 0;
+            }
             if (P.ablate & 32) hh[a] = (j * 0x9E3779B97F4A7C15ull) >> 22;   // timing only: no fetch/hash
         }
 #pragma unroll
@@ -540,10 +591,10 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
                 sj[pos] = (uint16_t)((br[q] >> 23) * L1_THREADS + threadIdx.x);
             }
         }
-        if (pre) {
+        if (!TW && pre) {
             const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
 #pragma unroll
-            for (int a = 0; a < KPT; a++) {
+            for (int a = 0; a < NPEND; a++) {
                 const uint64_t j = n0 + (uint64_t)a * L1_THREADS + threadIdx.x;
                 if (j < n1 && !(P.ablate & 32)) pend[a] = kmer_fetch(src, j);
             }
@@ -590,6 +641,7 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             }
             else tail[d] = v;   // the odd last record of the run (not on the last tile)
         }
+        if (TW && !last && threadIdx.x < L1F_TW) s_tw[((ti + 1) & 1) * L1F_TW + threadIdx.x] = tw_next;
         block_sync();
         for (uint32_t d = threadIdx.x; d < F1; d += blockDim.x) {
             const uint32_t h = hist[d];
