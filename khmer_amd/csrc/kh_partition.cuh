@@ -468,18 +468,16 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
     const uint32_t F1a = (F1 + 3) & ~3u;
     uint64_t *bcur = (uint64_t *)smem;                  // [F1] partially filled block (DEAD: overflowed)
     uint64_t *nbase = bcur + F1a;                       // [F1] blocks reserved for this tile
-    uint64_t *dla = nbase + F1a;                        // [F1] output - LDS position, current block
-    uint64_t *dlb = dla + F1a;                          // [F1] output - LDS position, new blocks
-    uint64_t *tail = dlb + F1a;                         // [F1] a pending odd record
+    uint64_t *dl = nbase + F1a;                         // [F1][2] output - LDS position: current block, new blocks
+    uint64_t *tail = dl + 2 * F1a;                      // [F1] a pending odd record
     uint32_t *stage = (uint32_t *)(tail + F1a);         // [TILE_RECS] bin offset inside the bucket
     uint32_t *cnt = stage + TILE_RECS;                  // [F1] records appended by this workgroup
     uint32_t *hist = cnt + F1a;                         // [F1]
     uint32_t *lstart = hist + F1a;                      // [F1]
-    uint32_t *qs = lstart + F1a;                        // [F1] first LDS position in the new blocks
-    uint32_t *qlim = qs + F1a;                          // [F1] first LDS position left for the tail
-    uint16_t *sb = (uint16_t *)(qlim + F1a);            // [TILE_RECS] bucket
-    uint16_t *sj = sb + TILE_RECS;                      // [TILE_RECS] k-mer index inside the tile
-    uint32_t *s_wtot = (uint32_t *)(sj + TILE_RECS);    // [16]
+    uint2 *qq = (uint2 *)(lstart + F1a);                // [F1] (first LDS position in the new blocks,
+                                                        //       first LDS position left for the tail)
+    uint32_t *sbj = (uint32_t *)(qq + F1a);             // [TILE_RECS] bucket << 16 | k-mer index inside the tile
+    uint32_t *s_wtot = sbj + TILE_RECS;                 // [16]
     uint64_t *s_meta = (uint64_t *)(s_wtot + 16);
     uint64_t *s_koff = s_meta + 2;
     // TW: fixed-length 2-bit reads whose tile spans <= L1F_TW words: the
@@ -587,8 +585,7 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
                 const uint32_t b = (br[q] >> 13) & 1023u;
                 const uint32_t pos = lstart[b] + (br[q] & 8191u);
                 stage[pos] = off[q];
-                sb[pos] = (uint16_t)b;
-                sj[pos] = (uint16_t)((br[q] >> 23) * L1_THREADS + threadIdx.x);
+                sbj[pos] = (b << 16) | ((br[q] >> 23) * L1_THREADS + threadIdx.x);
             }
         }
         if (!TW && pre) {
@@ -623,10 +620,9 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             const uint32_t q0 = lstart[d];
             const bool dead = bc == DEAD || nb == DEAD;
             nbase[d] = nb;
-            dla[d] = bc + (L0 & (BLK - 1)) - q0;
-            dlb[d] = nb + L0 - split - q0;
-            qs[d] = q0 + (split - L0);
-            qlim[d] = dead ? 0 : q0 + (fe > L0 ? fe - L0 : 0);
+            dl[2 * d] = bc + (L0 & (BLK - 1)) - q0;
+            dl[2 * d + 1] = nb + L0 - split - q0;
+            qq[d] = make_uint2(q0 + (split - L0), dead ? 0 : q0 + (fe > L0 ? fe - L0 : 0));
         }
         block_sync();
         const uint32_t ntile = lstart[F1 - 1] + hist[F1 - 1];
@@ -634,10 +630,11 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
         for (int u = 0; u < RPT; u++) {
             const uint32_t q = threadIdx.x + (uint32_t)u * L1_THREADS;
             if (q >= ntile) continue;
-            const uint32_t d = sb[q];
-            const uint64_t v = ((j0 + sj[q]) << 32) | stage[q];
-            if (q < qlim[d]) {
-                if (!(P.ablate & 16)) rec[(q < qs[d] ? dla[d] : dlb[d]) + q] = v;   // 16: timing only, no run writes
+            const uint32_t bj = sbj[q], d = bj >> 16;
+            const uint64_t v = ((j0 + (bj & 0xFFFFu)) << 32) | stage[q];
+            const uint2 ql = qq[d];   // (qs, qlim)
+            if (q < ql.y) {
+                if (!(P.ablate & 16)) rec[dl[2 * d + (q >= ql.x ? 1 : 0)] + q] = v;   // 16: timing only, no run writes
             }
             else tail[d] = v;   // the odd last record of the run (not on the last tile)
         }
