@@ -281,9 +281,30 @@ static uint32_t l1f_wpc(const Params &P) {
     const size_t regs = (l1f_rpt() == 8 ? L1F_WAVES_PER_EU : 4) * 4 / (L1_THREADS / 64);
     return (uint32_t)std::max<size_t>(1, std::min<size_t>(regs, 163840 / lds));
 }
+static bool use_own_filter(const Graph *g);
 static uint32_t l1f_workgroups(const Graph *g, uint64_t nkmers) {
     const uint64_t tiles = (nkmers + L1_THREADS - 1) / L1_THREADS;
-    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles / 8 + 1, (uint64_t)l1f_wpc(g->prm) * device_cus(g)));
+    const uint64_t wpc = use_own_filter(g) ? 2 : l1f_wpc(g->prm);   // k_own_l1f: ~75 KB of LDS
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles / 8 + 1, wpc * device_cus(g)));
+}
+static size_t lds_own_l1f(const Params &P) {
+    const size_t F1a = (P.F1 + 3) & ~3u;
+    return (size_t)2 * OWN_BATCH * 8 + F1a * 60 + (size_t)OWN_BATCH * 2 + 48 * 4;
+}
+// a shard's level 1 in one kernel (k_own_l1f) for fixed-length reads;
+// KH_OWN_L1F=0 falls back to k_own_filter + k_scatter_l1<PRE> (development)
+static bool own_l1f_on() { static const bool v = env_seg("KH_OWN_L1F", 1) != 0; return v; }
+template <class Src>
+using OwnL1FFn = void (*)(Params, Src, uint64_t, uint64_t, int, int, const uint64_t *, unsigned long long *,
+                          uint64_t *, uint64_t *, int);
+template <class Src>
+static OwnL1FFn<Src> own_l1f_kernel(int kpt) {
+    switch (kpt) {
+        case 1: return k_own_l1f<Src, 1>;
+        case 2: return k_own_l1f<Src, 2>;
+        case 4: return k_own_l1f<Src, 4>;
+        default: return k_own_l1f<Src, 8>;
+    }
 }
 template <class Src>
 using L1FFn = void (*)(Params, Src, uint64_t, uint64_t, int, int, const uint64_t *, unsigned long long *, uint64_t *,
@@ -668,9 +689,25 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     uint64_t nrec = 0;   // records this pass writes (exact level 1 only)
     for (;;) {
         l1f = fast && l1f_ok(g);
-        const uint64_t cap1 = l1f ? bkt_plan(g, nkmers) : 0;
+        const bool ownf = fast && !window && use_own_filter(g) && own_l1f_on();
+        const uint64_t cap1 = (l1f || ownf) ? bkt_plan(g, nkmers) : 0;
         // level 1
-        if (l1f) {
+        if (ownf) {
+            ensure_recs(g, std::max(cap1, cap2));
+            hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)((F1 + 255) / 256)), dim3(256), 0, st, w.bkt_base,
+                               (unsigned long long *)w.bkt_cur, (uint64_t)F1);
+            const uint32_t nwg = l1f_workgroups(g, nkmers);
+            for (int t0 = 0; t0 < P.n; t0 += 8) {
+                const int nt = std::min(8, P.n - t0);
+                int kpt = 1;
+                while (kpt * 2 * nt <= 8) kpt *= 2;
+                const uint64_t tk = (uint64_t)L1_THREADS * kpt;
+                const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
+                TIMED("own_l1f", hipLaunchKernelGGL(own_l1f_kernel<Src>(kpt), dim3(nwg), dim3(L1_THREADS),
+                                                    lds_own_l1f(P), st, P, src, nkmers, kpw, t0, nt, w.bkt_base,
+                                                    (unsigned long long *)w.bkt_cur, w.rec1, w.ctr, l1f_blk_sh()));
+            }
+        } else if (l1f) {
             ensure_recs(g, std::max(cap1, cap2));
             if (P.ablate & 16) KH_HIP(hipMemsetAsync(w.rec1, 0xFF, w.cap_recs * 8, st));   // timing only
             hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)((F1 + 255) / 256)), dim3(256), 0, st, w.bkt_base,
@@ -734,15 +771,16 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                                                        src, nkmers, q.ck1, q.nch1, t0, nt, w.moff, w.rec1));
             }
         }
-        if (check_mode() && !l1f) check_holes(g, w.rec1, nrec, "scatter_l1");
+        if (check_mode() && !l1f && !ownf) check_holes(g, w.rec1, nrec, "scatter_l1");
         // level 2
         if (fast) {
             const uint64_t nreg = F1 * F2;
             const uint32_t parts = l2f_parts((uint32_t)F1);
             hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)std::min<uint64_t>((nreg + 255) / 256, 4096)), dim3(256), 0,
                                st, w.reg_base, (unsigned long long *)w.reg_cur, nreg);
-            const uint64_t *bs = l1f ? w.bkt_base : w.off1;
-            const uint64_t *be = l1f ? w.bkt_cur : w.off1 + 1;
+            const bool bkt = l1f || ownf;   // level 1 went into fixed-capacity buckets
+            const uint64_t *bs = bkt ? w.bkt_base : w.off1;
+            const uint64_t *be = bkt ? w.bkt_cur : w.off1 + 1;
             static const int l2rpt = env_seg("KH_L2_RPT", L2_RPT);   // development: 8 or 16
             TIMED("scatter_l2", hipLaunchKernelGGL((l2rpt == 16 ? k_scatter_l2f<PT_THREADS, 16> : k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(F1 * parts)),
                                                    dim3(PT_THREADS), lds_scatter_l2f(P), st, (uint32_t)F1, P.s0, P.s2,
@@ -1357,6 +1395,11 @@ static void set_lds_limits() {
             KH_LDS_MAX(l1f_kernel<SrcHashes>(kpt, rpt));
         }
     KH_LDS_MAX((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>));
+    for (int kpt : {1, 2, 4, 8}) {
+        KH_LDS_MAX(own_l1f_kernel<SrcTwoBit>(kpt));
+        KH_LDS_MAX(own_l1f_kernel<SrcBytes>(kpt));
+        KH_LDS_MAX(own_l1f_kernel<SrcHashes>(kpt));
+    }
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 1>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 2>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 4>));

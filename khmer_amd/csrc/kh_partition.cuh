@@ -779,6 +779,214 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_filter(Params P, Src src, ui
     if (nb) flush(nb);
 }
 
+// Level 1 of a shard in one kernel: k_own_filter's owned-record filter feeding
+// k_scatter_l1f's fixed-capacity bucket placement.  Each filter tile hashes
+// KPT k-mers per thread and appends the owned records (j << 32 | local bin)
+// to an LDS buffer; whenever it holds OWN_BATCH records they are
+// counting-sorted by bucket in LDS and appended to the workgroup's blocks
+// exactly as in k_scatter_l1f (2-record tails, one returning atomic per
+// (bucket, batch, new block)).  The owned records never make the round trip
+// through HBM that k_own_filter + k_hist_rec + k_scatter_l1<PRE> take.
+constexpr int OWN_BATCH = L1_THREADS * 8;   // records sorted per batch
+template <class Src, int KPT>
+__global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint64_t nkmers, uint64_t kpw, int t0,
+                                                       int nt, const uint64_t *bkt_base, unsigned long long *bkt_cur,
+                                                       uint64_t *rec, uint64_t *ctr, int blk_sh) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int RPT = 8;
+    constexpr int FSLOTS = 8;                          // candidate records per thread per filter tile
+    constexpr int TPK = FSLOTS / KPT;                  // table slots per k-mer
+    constexpr int TILE_KMERS = L1_THREADS * KPT;
+    static_assert(L1_THREADS * FSLOTS <= OWN_BATCH, "a filter tile must fit the buffer's second half");
+    const uint32_t BLK = 1u << blk_sh;
+    constexpr uint64_t DEAD = ~0ull;
+    const uint32_t F1 = P.F1;
+    const uint32_t F1a = (F1 + 3) & ~3u;
+    uint64_t *buf = (uint64_t *)smem;                  // [2 * OWN_BATCH] owned records; [0, OWN_BATCH) is the stage while sorting
+    uint64_t *bcur = buf + 2 * OWN_BATCH;              // [F1] partially filled block (DEAD: overflowed)
+    uint64_t *nbase = bcur + F1a;                      // [F1] blocks reserved for this batch
+    uint64_t *dl = nbase + F1a;                        // [F1][2] output - LDS position: current block, new blocks
+    uint64_t *tail = dl + 2 * F1a;                     // [F1] a pending odd record
+    uint32_t *cnt = (uint32_t *)(tail + F1a);          // [F1] records appended by this workgroup
+    uint32_t *hist = cnt + F1a;                        // [F1]
+    uint32_t *lstart = hist + F1a;                     // [F1]
+    uint2 *qq = (uint2 *)(lstart + F1a);               // [F1] (first LDS position in the new blocks, first left for the tail)
+    uint16_t *sb = (uint16_t *)(qq + F1a);             // [OWN_BATCH] bucket of each stage slot
+    uint32_t *s_wtot = (uint32_t *)(sb + OWN_BATCH);   // [3][16]: filter scans (tile parity), batch scan
+    const int shift = P.s0 + P.s2;
+    const uint64_t omask = (1ull << shift) - 1;
+    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) {
+        bcur[b] = 0;
+        cnt[b] = 0;
+        hist[b] = 0;
+    }
+    const uint64_t c0 = min(nkmers, (uint64_t)blockIdx.x * kpw);
+    const uint64_t c1 = min(nkmers, c0 + kpw);
+    typename Src::Pend pend[KPT];
+#pragma unroll
+    for (int a = 0; a < KPT; a++) {
+        const uint64_t j = c0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+        if (j < min(c1, c0 + TILE_KMERS)) pend[a] = kmer_fetch(src, j);
+    }
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nwaves = blockDim.x >> 6;
+
+    // sort buf[0, n) by bucket and append it (last: flush every pending tail)
+    auto sort_batch = [&](uint32_t n, bool last) {
+        uint32_t off[RPT], br[RPT], jv[RPT];
+#pragma unroll
+        for (int u = 0; u < RPT; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * L1_THREADS;
+            off[u] = ~0u;
+            br[u] = 0;
+            jv[u] = 0;
+            if (q < n) {
+                const uint64_t x = buf[q];
+                const uint32_t G = (uint32_t)x, b = G >> shift;
+                off[u] = G & (uint32_t)omask;
+                jv[u] = (uint32_t)(x >> 32);
+                br[u] = (b << 13) | atomicAdd(&hist[b], 1u);
+            }
+        }
+        block_sync();   // every record is in registers: buf[0, OWN_BATCH) becomes the stage
+        block_scan_hist(hist, lstart, F1, s_wtot + 32);
+        block_sync();
+#pragma unroll
+        for (int u = 0; u < RPT; u++) {
+            if (off[u] != ~0u) {
+                const uint32_t b = br[u] >> 13;
+                const uint32_t pos = lstart[b] + (br[u] & 8191u);
+                buf[pos] = ((uint64_t)jv[u] << 32) | off[u];
+                sb[pos] = (uint16_t)b;
+            }
+        }
+        for (uint32_t d = threadIdx.x; d < F1; d += blockDim.x) {
+            const uint32_t h = hist[d];
+            if (!h && !last) continue;
+            const uint32_t L0 = cnt[d];
+            const uint32_t split = (L0 + BLK - 1) & ~(BLK - 1);
+            const uint32_t need = ((L0 + h + BLK - 1) >> blk_sh) - (split >> blk_sh);
+            uint64_t bc = bcur[d], nb = 0;
+            if (bc == DEAD) {
+                nb = DEAD;
+            } else if (need) {
+                nb = atomicAdd(&bkt_cur[d], (unsigned long long)need * BLK);
+                if (nb + (uint64_t)need * BLK > bkt_base[d + 1]) {
+                    atomicOr((unsigned long long *)&ctr[CTR_ERR], 8ull);
+                    nb = DEAD;
+                }
+            }
+            const uint32_t e = L0 + h, fe = last ? e : (e & ~1u);
+            if ((L0 & 1) && fe > L0 - 1 && bc != DEAD) rec[bc + ((L0 - 1) & (BLK - 1))] = tail[d];
+            const uint32_t q0 = lstart[d];
+            const bool dead = bc == DEAD || nb == DEAD;
+            nbase[d] = nb;
+            dl[2 * d] = bc + (L0 & (BLK - 1)) - q0;
+            dl[2 * d + 1] = nb + L0 - split - q0;
+            qq[d] = make_uint2(q0 + (split - L0), dead ? 0 : q0 + (fe > L0 ? fe - L0 : 0));
+        }
+        block_sync();
+#pragma unroll
+        for (int u = 0; u < RPT; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * L1_THREADS;
+            if (q >= n) continue;
+            const uint32_t d = sb[q];
+            const uint64_t v = buf[q];
+            const uint2 ql = qq[d];
+            if (q < ql.y) rec[dl[2 * d + (q >= ql.x ? 1 : 0)] + q] = v;
+            else tail[d] = v;   // the odd last record of the run (not on the last batch)
+        }
+        block_sync();
+        for (uint32_t d = threadIdx.x; d < F1; d += blockDim.x) {
+            const uint32_t h = hist[d];
+            if (!h) continue;
+            const uint32_t L0 = cnt[d];
+            const uint32_t need = ((L0 + h + BLK - 1) >> blk_sh) - ((L0 + BLK - 1) >> blk_sh);
+            if (nbase[d] == DEAD) bcur[d] = DEAD;
+            else if (need) bcur[d] = nbase[d] + (uint64_t)(need - 1) * BLK;
+            cnt[d] = L0 + h;
+            hist[d] = 0;
+        }
+        block_sync();
+    };
+
+    uint32_t nbuf = 0;   // records in buf (block-uniform)
+    bool flushed_last = false;
+    const uint32_t ntiles = uniform_u32((uint32_t)((c1 - c0 + TILE_KMERS - 1) / TILE_KMERS));
+    for (uint32_t ti = 0; ti < ntiles; ti++) {
+        const uint64_t j0 = c0 + (uint64_t)ti * TILE_KMERS;
+        const uint64_t j1 = min(c1, j0 + TILE_KMERS);
+        uint64_t v[FSLOTS];
+        uint32_t own = 0;   // bit q: record slot q is owned here
+        uint64_t hh[KPT];
+#pragma unroll
+        for (int a = 0; a < KPT; a++) {
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            hh[a] = j < j1 ? src.finish(pend[a]) : 0;
+        }
+        {
+            const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
+#pragma unroll
+            for (int a = 0; a < KPT; a++) {
+                const uint64_t j = n0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+                if (j < n1) pend[a] = kmer_fetch(src, j);
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < KPT; a++) {
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+#pragma unroll
+            for (int i = 0; i < TPK; i++) {
+                uint64_t G;
+                if (i < nt && j < j1 && local_bin(P, t0 + i, hh[a], &G)) {
+                    v[a * TPK + i] = (j << 32) | G;
+                    own |= 1u << (a * TPK + i);
+                }
+            }
+        }
+        // tile-wide exclusive scan of the per-thread counts
+        uint32_t *wt = s_wtot + (ti & 1) * 16;
+        const uint32_t c = __builtin_popcount(own);
+        uint32_t incl = c;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= (uint32_t)d) incl += y;
+        }
+        if (lane == 63) wt[wave] = incl;
+        block_sync();
+        uint32_t tot = 0, pos = incl - c;
+        for (uint32_t w = 0; w < nwaves; w++) {
+            const uint32_t x = wt[w];
+            tot += x;
+            if (w < wave) pos += x;
+        }
+        tot = uniform_u32(tot);
+        pos += nbuf;
+#pragma unroll
+        for (int q = 0; q < FSLOTS; q++)
+            if ((own >> q) & 1) buf[pos + __builtin_popcount(own & ((1u << q) - 1))] = v[q];
+        nbuf += tot;
+        block_sync();
+        const bool lt = ti + 1 == ntiles;
+        while (nbuf >= (uint32_t)OWN_BATCH || (lt && !flushed_last)) {
+            const uint32_t n = min(nbuf, (uint32_t)OWN_BATCH);
+            const bool last = lt && nbuf == n;
+            sort_batch(n, last);
+            flushed_last = last;
+            for (uint32_t x = threadIdx.x; x < nbuf - n; x += blockDim.x) buf[x] = buf[n + x];   // leftover to the front
+            nbuf -= n;
+            block_sync();
+        }
+    }
+    block_sync();
+    for (uint32_t y = threadIdx.x; y < F1 * BLK; y += blockDim.x) {
+        const uint32_t d = y >> blk_sh, sl = y & (BLK - 1);
+        const uint32_t c = cnt[d] & (BLK - 1);
+        if (c == 0 || sl < c || bcur[d] == DEAD) continue;
+        rec[bcur[d] + sl] = ~0ull;
+    }
+}
+
 // per-chunk bucket histogram of a flat record stream: chunk c = records
 // [c * L2_CHUNK, ...), destination (uint32)record >> shift; M[d * nch + c]
 __global__ void __launch_bounds__(PT_THREADS) k_hist_rec(const uint64_t *rec, uint64_t n, uint32_t F, int shift,
