@@ -32,6 +32,14 @@ void parser_fill_batch(Parser *p, HostBatch &b, int k, uint64_t max_kmers, uint6
                        uint64_t *taken);
 void parser_fill_raw(Parser *p, RawBatch &b, int k, uint64_t max_kmers, uint64_t max_bases, bool *done,
                      uint64_t *taken);
+struct PlainFile;
+PlainFile *parser_plain_open(Parser *pr);
+void parser_plain_close(PlainFile *f);
+size_t plain_size(const PlainFile *f);
+size_t plain_record_start(const PlainFile *f, size_t from);
+uint64_t plain_parse_range(const PlainFile *f, size_t start, size_t stop, int k, uint64_t max_kmers,
+                           std::vector<RawBatch> &out, uint64_t *nreads);
+void parser_mark_drained(Parser *pr, uint64_t nreads);
 void engine_hash_batch(Graph *g, const HostBatch &b, uint64_t *h_out);
 void engine_synth_packed(int device, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L, int k,
                          uint64_t *d_words, uint64_t *d_koff);
@@ -308,7 +316,150 @@ struct FeedSlot {
     HostBatch packed;
     bool ready = false;
 };
+static void pack_raw(const RawBatch &raw, HostBatch &b, int k, int hash) {
+    b.hash = hash;
+    const char *p = raw.seq.data();
+    for (uint32_t n : raw.len) {
+        b.append(p, n, k, true);
+        p += n;
+    }
+}
+
+// Chunk-parallel feed of a plain file (kh_parser.cpp parser_plain_open):
+// worker threads parse and pack chunks of ~64 MB cut at record starts; the
+// calling thread consumes them in file order after checking that each chunk
+// starts where the previous one really ended (otherwise it parses the rest
+// of the file itself, serially).  Same reads, same order, same errors as the
+// serial parser.
+static void consume_chunked(Graph *g, Parser *parser, PlainFile *pf, uint64_t *nreads_out, uint64_t *consumed) {
+    struct Chunk {
+        std::vector<RawBatch> raw;
+        std::vector<HostBatch> packed;
+        uint64_t nreads = 0, start = 0, end = 0;
+        std::exception_ptr err;
+        bool ready = false;
+    };
+    const size_t n = plain_size(pf);
+    const char *ce = getenv("KH_FEED_CHUNK");   // development / tests: chunk bytes
+    const size_t CH = ce && atoll(ce) > 0 ? (size_t)atoll(ce) : (size_t)64 << 20;
+    const size_t nch = (n + CH - 1) / CH;
+    const int T = std::max(1, feed_threads() - 1);
+    const size_t depth = (size_t)T * 2;
+    const uint64_t maxk = std::min<uint64_t>(g->batch_kmers, 1ull << 27);
+    const int k = g->k, hash = g->hash;
+    std::vector<std::unique_ptr<Chunk>> ch(nch);
+    for (auto &c : ch) c.reset(new Chunk());
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t next = 0, taken_upto = 0;   // next chunk to parse; chunks below taken_upto are consumed
+    bool stop = false;
+    std::vector<std::thread> workers;
+    for (int t = 0; t < T; t++)
+        workers.emplace_back([&] {
+            for (;;) {
+                size_t c;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return stop || next >= nch || next < taken_upto + depth; });
+                    if (stop || next >= nch) return;
+                    c = next++;
+                }
+                Chunk &C = *ch[c];
+                try {
+                    C.start = plain_record_start(pf, c * CH);
+                    const size_t stop_at = c + 1 < nch ? plain_record_start(pf, (c + 1) * CH) : n;
+                    C.end = C.start < n ? plain_parse_range(pf, C.start, stop_at, k, maxk, C.raw, &C.nreads) : n;
+                } catch (...) {
+                    C.err = std::current_exception();
+                }
+                for (const RawBatch &r : C.raw) {
+                    C.packed.emplace_back();
+                    pack_raw(r, C.packed.back(), k, hash);
+                }
+                std::vector<RawBatch>().swap(C.raw);
+                std::lock_guard<std::mutex> lk(mu);
+                C.ready = true;
+                cv.notify_all();
+            }
+        });
+    auto finish = [&] {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+            cv.notify_all();
+        }
+        for (auto &t : workers) t.join();
+    };
+    uint64_t total = 0;
+    size_t true_end = 0;   // where the reads consumed so far really end
+    bool serial_rest = false;
+    try {
+        for (size_t c = 0; c < nch; c++) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return ch[c]->ready; });
+            }
+            Chunk &C = *ch[c];
+            if (C.start != true_end && !(C.start >= n && true_end >= n)) {   // a chunk start that was not a record start
+                serial_rest = true;
+                break;
+            }
+            for (HostBatch &b : C.packed) {
+                if (b.nkmers()) engine_consume_host(g, b, nullptr);
+                *consumed += b.nkmers();
+                HostBatch().words.swap(b.words);
+            }
+            total += C.nreads;
+            true_end = C.end;
+            if (C.err) {
+                *nreads_out = total;
+                parser_mark_drained(parser, total);
+                std::rethrow_exception(C.err);
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                taken_upto = c + 1;
+                cv.notify_all();
+            }
+            C.packed.clear();
+        }
+    } catch (...) {
+        finish();
+        throw;
+    }
+    finish();
+    if (serial_rest && true_end < n) {
+        std::vector<RawBatch> raw;
+        uint64_t nr = 0;
+        std::exception_ptr err;
+        try {
+            plain_parse_range(pf, true_end, n, k, maxk, raw, &nr);
+        } catch (...) {
+            err = std::current_exception();
+        }
+        for (const RawBatch &r : raw) {
+            HostBatch b;
+            pack_raw(r, b, k, hash);
+            if (b.nkmers()) engine_consume_host(g, b, nullptr);
+            *consumed += b.nkmers();
+        }
+        total += nr;
+        if (err) {
+            *nreads_out = total;
+            parser_mark_drained(parser, total);
+            std::rethrow_exception(err);
+        }
+    }
+    *nreads_out = total;
+    parser_mark_drained(parser, total);
+}
+
 static void consume_pipelined(Graph *g, Parser *parser, uint64_t *nreads_out, uint64_t *consumed) {
+    if (PlainFile *pf = parser_plain_open(parser)) {
+        std::unique_ptr<PlainFile, void (*)(PlainFile *)> hold(pf, parser_plain_close);
+        consume_chunked(g, parser, pf, nreads_out, consumed);
+        return;
+    }
     const int T = feed_threads();
     const int npack = std::max(1, T - 1);
     const int depth = npack + 2;                       // batches in flight

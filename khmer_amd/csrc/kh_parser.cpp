@@ -30,8 +30,13 @@
 #include <ctype.h>
 #include <stdio.h>
 #include <string.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <memory>
 #include <string>
 
@@ -63,6 +68,7 @@ constexpr int BZ_OK_ = 0, BZ_STREAM_END_ = 4;
 struct Source {
     std::string path;
     virtual ~Source() {}
+    virtual bool plain() const { return false; }   // uncompressed file read as is
     // up to n bytes into dst; 0 at the clean end of the stream; throws on a
     // corrupt or truncated stream
     virtual size_t read(unsigned char *dst, size_t n) = 0;
@@ -74,6 +80,7 @@ struct Source {
 struct GzSource : Source {
     gzFile gz = nullptr;
     ~GzSource() override { if (gz) gzclose(gz); }
+    bool plain() const override { return gz && gzdirect(gz) == 1; }
     size_t read(unsigned char *dst, size_t n) override {
         int got = gzread(gz, dst, (unsigned)n);
         if (got > 0) return (size_t)got;
@@ -133,6 +140,18 @@ struct Bz2Source : Source {
     }
 };
 
+// bytes [pos, n) of a mapped file, read on demand (chunk parsers)
+struct MemSource : Source {
+    const unsigned char *p = nullptr;
+    size_t n = 0, pos = 0;
+    size_t read(unsigned char *dst, size_t m) override {
+        const size_t k = std::min(m, n - pos);
+        memcpy(dst, p + pos, k);
+        pos += k;
+        return k;
+    }
+};
+
 std::unique_ptr<Source> open_source(const char *path) {
     unsigned char magic[3] = {0, 0, 0};
     FILE *f = fopen(path, "rb");
@@ -182,12 +201,16 @@ struct Parser {
 
     std::string broken;   // a corrupt stream met while opening, raised on first use
 
+    uint64_t src_bytes = 0;   // bytes taken from src so far
+    // offset of the next unparsed byte in the source's stream
+    uint64_t offset() const { return src_bytes - (len - pos); }
     int peek() {
         if (pos < len) return buf[pos];
         if (!broken.empty()) fail(KH_EFILE, broken);
         if (eof) return -1;
         size_t n = src->read(buf.data(), buf.size());
         if (n == 0) { eof = true; len = pos = 0; return -1; }
+        src_bytes += n;
         len = n; pos = 0;
         return buf[0];
     }
@@ -343,6 +366,141 @@ void parser_fill_batch(Parser *p, HostBatch &b, int k, uint64_t max_kmers, uint6
         (*taken)++;
         if (p->seq.size() >= (size_t)k) b.append(p->seq.data(), p->seq.size(), k, true);
     }
+}
+
+// ---- chunk-parallel parsing of plain files (kh_capi.cpp consume_pipelined) ----
+// A plain FASTA/FASTQ file that no read has been taken from yet is mapped and
+// cut into chunks at record starts; each chunk is parsed by its own Parser
+// over the mapped bytes (the same record semantics), so parsing scales with
+// threads.  A chunk start is a line beginning with '>' (FASTA: unambiguous) or
+// with '@' that begins two consecutive well-formed four-line records (FASTQ).
+// Chunk c's parser stops at the first record boundary at or past chunk c+1's
+// start; the consumer checks that they coincide and otherwise re-parses the
+// rest of the file serially from where chunk c really ended (exact either way).
+struct PlainFile {
+    std::string path;
+    int fd = -1;
+    const unsigned char *p = nullptr;
+    size_t n = 0;
+    bool fastq = false;
+    ~PlainFile() {
+        if (p) munmap((void *)p, n);
+        if (fd >= 0) close(fd);
+    }
+};
+
+PlainFile *parser_plain_open(Parser *pr) {
+    std::lock_guard<std::mutex> lk(pr->mu);
+    if (pr->num_reads != 0 || pr->offset() != 0 || !pr->broken.empty() || !pr->src->plain()) return nullptr;
+    std::unique_ptr<PlainFile> f(new PlainFile());
+    f->path = pr->path;
+    f->fastq = pr->fastq;
+    f->fd = open(pr->path.c_str(), O_RDONLY);
+    if (f->fd < 0) return nullptr;
+    struct stat st;
+    if (fstat(f->fd, &st) != 0 || st.st_size <= 0) return nullptr;
+    f->n = (size_t)st.st_size;
+    void *m = mmap(nullptr, f->n, PROT_READ, MAP_PRIVATE, f->fd, 0);
+    if (m == MAP_FAILED) return nullptr;
+    f->p = (const unsigned char *)m;
+    madvise(m, f->n, MADV_SEQUENTIAL);
+    return f.release();
+}
+void parser_plain_close(PlainFile *f) { delete f; }
+size_t plain_size(const PlainFile *f) { return f->n; }
+
+// the first record start at or after `from` (f->n if none)
+size_t plain_record_start(const PlainFile *f, size_t from) {
+    const unsigned char *p = f->p, *e = f->p + f->n;
+    if (from == 0) return 0;
+    auto line_end = [&](const unsigned char *q) -> const unsigned char * {
+        const void *x = memchr(q, '\n', (size_t)(e - q));
+        return x ? (const unsigned char *)x : e;
+    };
+    // start of the first line beginning at or after from
+    const unsigned char *q = p + from;
+    if (q[-1] != '\n') {
+        q = line_end(q);
+        if (q < e) q++;
+    }
+    auto record4 = [&](const unsigned char *r, const unsigned char **next) -> bool {
+        if (r >= e || *r != '@') return false;
+        const unsigned char *l1 = line_end(r);
+        if (l1 >= e) return false;
+        const unsigned char *s0 = l1 + 1, *s1 = line_end(s0);
+        if (s1 >= e || s1 == s0) return false;
+        const unsigned char *p0 = s1 + 1;
+        if (p0 >= e || *p0 != '+') return false;
+        const unsigned char *p1 = line_end(p0);
+        if (p1 >= e) return false;
+        const unsigned char *q0 = p1 + 1, *q1 = line_end(q0);
+        if (q1 - q0 != s1 - s0) return false;
+        for (const unsigned char *c = s0; c < s1; c++)
+            if (*c == '\r' || *c == ' ' || *c == '\t') return false;
+        for (const unsigned char *c = q0; c < q1; c++)
+            if (*c == '\r' || *c == ' ' || *c == '\t') return false;
+        *next = q1 < e ? q1 + 1 : e;
+        return true;
+    };
+    while (q < e) {
+        if (!f->fastq) {
+            if (*q == '>') return (size_t)(q - p);
+        } else if (*q == '@') {
+            const unsigned char *n1, *n2;
+            if (record4(q, &n1) && (n1 >= e || record4(n1, &n2))) return (size_t)(q - p);
+        }
+        q = line_end(q);
+        if (q < e) q++;
+    }
+    return f->n;
+}
+
+// Parse records starting at byte `start` until the next record would start at
+// or past `stop`; returns the offset where parsing stopped.  Reads >= k bases
+// go into raw batches of <= max_kmers k-mers (out grows by one batch at a
+// time).  *nreads counts good reads; a malformed record throws after the
+// reads before it are in out.
+uint64_t plain_parse_range(const PlainFile *f, size_t start, size_t stop, int k, uint64_t max_kmers,
+                           std::vector<RawBatch> &out, uint64_t *nreads) {
+    Parser pr;
+    std::unique_ptr<MemSource> ms(new MemSource());
+    ms->path = f->path;
+    ms->p = f->p;
+    ms->n = f->n;
+    ms->pos = start;
+    pr.src = std::move(ms);
+    pr.path = f->path;
+    pr.buf.resize(1 << 22);
+    pr.fastq = f->fastq;
+    pr.have_qualities = f->fastq;
+    pr.num_reads = 1;   // the first-read rule (have_qualities) was settled by the file's first record
+    if (out.empty()) out.emplace_back();
+    for (;;) {
+        if (start + pr.offset() >= stop) break;
+        if (pr.next_read_locked() == KH_END) break;
+        (*nreads)++;
+        const size_t n = pr.seq.size();
+        if (n < (size_t)k) continue;
+        RawBatch *b = &out.back();
+        if (b->nkmers >= max_kmers) {
+            out.emplace_back();
+            b = &out.back();
+        }
+        b->seq.insert(b->seq.end(), pr.seq.begin(), pr.seq.end());
+        b->len.push_back((uint32_t)n);
+        b->nkmers += n - (size_t)k + 1;
+        b->nreads_parsed++;
+    }
+    return start + pr.offset();
+}
+
+// the parser has been drained by the chunk path: reads counted, nothing left
+void parser_mark_drained(Parser *pr, uint64_t nreads) {
+    std::lock_guard<std::mutex> lk(pr->mu);
+    pr->num_reads += nreads;
+    pr->eof = true;
+    pr->pos = pr->len = 0;
+    pr->src.reset(new MemSource());
 }
 
 // Raw reads (uncleaned sequence bytes) of up to max_kmers k-mers for the
