@@ -186,7 +186,13 @@ static void ensure_recs(Graph *g, uint64_t recs) {
 static int env_seg(const char *name, int dflt);
 static int l1f_blk_sh() { static const int v = env_seg("KH_L1F_BLK_SH", L1F_BLK_SH); return v; }
 static int l2f_blk_sh() { static const int v = env_seg("KH_L2F_BLK_SH", L2F_BLK_SH); return v; }
-static uint32_t l2f_parts(uint32_t F1) { return std::max<uint32_t>(1, std::min<uint32_t>(16, (2048 + F1 - 1) / F1)); }
+static uint32_t l2f_parts(uint32_t F1) {
+    static const int v = env_seg("KH_L2F_PARTS", 0);   // development: workgroups per bucket
+    if (v > 0) return (uint32_t)v;
+    // ~8K workgroups: few buckets' regions are written at once (measured: 32
+    // per bucket at C2 beats 8 by 3 ms/step, at ~3 % more partial blocks)
+    return std::max<uint32_t>(1, std::min<uint32_t>(32, (8192 + F1 - 1) / F1));
+}
 static size_t lds_scatter_l2f(const Params &P) { return ((size_t)1 << P.s2) * (8 + 8 + 16 * 8 + 4 + 4 + 2) + 16; }
 
 // The fixed-capacity path is used when a full region expects >= 512 records
