@@ -275,8 +275,8 @@ static int l1f_rpt() { static const int v = env_seg("KH_L1F_RPT", L1_MAX_RPT) ==
 static size_t lds_scatter_l1f(const Params &P, bool window, int tile_kmers) {
     const size_t F1a = (P.F1 + 3) & ~3u;
     const size_t tile = (size_t)L1_THREADS * l1f_rpt();
-    return F1a * 8 * 5 + tile * 4 + F1a * 4 * 5 + tile * 2 * 2 + 64 + lds_window(window, tile_kmers) +
-           2 * L1F_TW * 8;
+    return F1a * 8 * 5 + (tile + 2 * F1a) * 4 + F1a * 4 * 5 + (tile + 2 * F1a) * 4 + 64 +
+           lds_window(window, tile_kmers) + 2 * L1F_TW * 8;
 }
 // as many workgroups per CU as the LDS allows, up to the kernel's register
 // budget (3 at 8 records per thread, 2 at 16); KH_L1F_WPC overrides (development)

@@ -450,7 +450,7 @@ __host__ __device__ constexpr size_t l1f_tw_offset(size_t F1a, int rpt) {
     // u64 index: 5 F1a u64 arrays, then (stage u32 + sb u16 + sj u16) per
     // record, 5 F1a u32 arrays, s_wtot, s_meta, s_koff (the window, unused
     // for fixed-length reads) rounded to 8 bytes
-    return (F1a * 8 * 5 + (size_t)L1_THREADS * rpt * 8 + F1a * 4 * 5 + 64 + 16 + 7) / 8;
+    return (F1a * 8 * 5 + ((size_t)L1_THREADS * rpt + 2 * F1a) * 8 + F1a * 4 * 5 + 64 + 16 + 7) / 8;
 }
 
 template <class Src, int KPT, int RPT_ = L1_MAX_RPT, bool TW_ = false>
@@ -470,14 +470,19 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
     uint64_t *nbase = bcur + F1a;                       // [F1] blocks reserved for this tile
     uint64_t *dl = nbase + F1a;                         // [F1][2] output - LDS position: current block, new blocks
     uint64_t *tail = dl + 2 * F1a;                      // [F1] a pending odd record
-    uint32_t *stage = (uint32_t *)(tail + F1a);         // [TILE_RECS] bin offset inside the bucket
-    uint32_t *cnt = stage + TILE_RECS;                  // [F1] records appended by this workgroup
+    // stage slots: TILE_RECS records + per bucket at most one leading hole
+    // and one trailing pad (every bucket's run starts on an even slot, so
+    // stage slot pairs map onto 16-B aligned output record pairs)
+    const uint32_t NSLOT = TILE_RECS + 2 * F1a;
+    uint32_t *stage = (uint32_t *)(tail + F1a);         // [NSLOT] bin offset inside the bucket
+    uint32_t *cnt = stage + NSLOT;                      // [F1] records appended by this workgroup
     uint32_t *hist = cnt + F1a;                         // [F1]
     uint32_t *lstart = hist + F1a;                      // [F1]
     uint2 *qq = (uint2 *)(lstart + F1a);                // [F1] (first LDS position in the new blocks,
                                                         //       first LDS position left for the tail)
-    uint32_t *sbj = (uint32_t *)(qq + F1a);             // [TILE_RECS] bucket << 16 | k-mer index inside the tile
-    uint32_t *s_wtot = sbj + TILE_RECS;                 // [16]
+    uint32_t *sbj = (uint32_t *)(qq + F1a);             // [NSLOT] bucket << 16 | k-mer index in the tile (SLOT_EMPTY: hole / pad)
+    uint32_t *s_wtot = sbj + NSLOT;                     // [16]
+    constexpr uint32_t SLOT_EMPTY = 0xFFFFu;
     uint64_t *s_meta = (uint64_t *)(s_wtot + 16);
     uint64_t *s_koff = s_meta + 2;
     // TW: fixed-length 2-bit reads whose tile spans <= L1F_TW words: the
@@ -577,13 +582,21 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             }
         }
         block_sync();
-        block_scan_hist(hist, lstart, F1, s_wtot);
+        // stage region of bucket d: an even number of slots, a leading hole
+        // when a record of the bucket is pending (its pair partner), the run,
+        // a trailing pad when the run ends unpaired
+        for (uint32_t d = threadIdx.x; d < F1; d += blockDim.x) {
+            const uint32_t h = hist[d];
+            lstart[d] = h ? (h + (cnt[d] & 1u) + 1u) & ~1u : 0u;
+        }
+        block_sync();
+        block_scan_hist(lstart, lstart, F1, s_wtot);   // in place: region starts (even)
         block_sync();
 #pragma unroll
         for (int q = 0; q < RPT; q++) {
             if (off[q] != ~0u) {
                 const uint32_t b = (br[q] >> 13) & 1023u;
-                const uint32_t pos = lstart[b] + (br[q] & 8191u);
+                const uint32_t pos = lstart[b] + (cnt[b] & 1u) + (br[q] & 8191u);
                 stage[pos] = off[q];
                 sbj[pos] = (b << 16) | ((br[q] >> 23) * L1_THREADS + threadIdx.x);
             }
@@ -617,7 +630,11 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             }
             const uint32_t e = L0 + h, fe = last ? e : (e & ~1u);
             if ((L0 & 1) && fe > L0 - 1 && bc != DEAD) rec[bc + ((L0 - 1) & (BLK - 1))] = tail[d];
-            const uint32_t q0 = lstart[d];
+            const uint32_t q0 = lstart[d] + (L0 & 1);   // the run's first slot (odd after a hole)
+            if (h) {
+                if (L0 & 1) sbj[q0 - 1] = (d << 16) | SLOT_EMPTY;
+                if ((q0 + h) & 1) sbj[q0 + h] = (d << 16) | SLOT_EMPTY;
+            }
             const bool dead = bc == DEAD || nb == DEAD;
             nbase[d] = nb;
             dl[2 * d] = bc + (L0 & (BLK - 1)) - q0;
@@ -625,18 +642,33 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             qq[d] = make_uint2(q0 + (split - L0), dead ? 0 : q0 + (fe > L0 ? fe - L0 : 0));
         }
         block_sync();
-        const uint32_t ntile = lstart[F1 - 1] + hist[F1 - 1];
-#pragma unroll
-        for (int u = 0; u < RPT; u++) {
-            const uint32_t q = threadIdx.x + (uint32_t)u * L1_THREADS;
-            if (q >= ntile) continue;
-            const uint32_t bj = sbj[q], d = bj >> 16;
-            const uint64_t v = ((j0 + (bj & 0xFFFFu)) << 32) | stage[q];
-            const uint2 ql = qq[d];   // (qs, qlim)
-            if (q < ql.y) {
-                if (!(P.ablate & 16)) rec[dl[2 * d + (q >= ql.x ? 1 : 0)] + q] = v;   // 16: timing only, no run writes
+        // write-out by slot pairs: a pair of records is one 16-B store (its
+        // output position is even, inside one block); a (hole, record) or
+        // (record, pad) pair writes its record alone, or parks it in the
+        // bucket's tail when it is the run's unpaired last (not on the last tile)
+        {
+            const uint32_t dlast = F1 - 1;
+            const uint32_t nslot = lstart[dlast] + (hist[dlast] ? (hist[dlast] + (cnt[dlast] & 1u) + 1u) & ~1u : 0u);
+            const uint2 *sbj2 = (const uint2 *)sbj;
+            const uint2 *stage2 = (const uint2 *)stage;
+            for (uint32_t m = threadIdx.x; 2 * m < nslot; m += L1_THREADS) {
+                const uint32_t q = 2 * m;
+                const uint2 bj = sbj2[m], st = stage2[m];
+                const uint32_t d = bj.x >> 16;
+                const bool r0 = (bj.x & 0xFFFFu) != SLOT_EMPTY, r1 = (bj.y & 0xFFFFu) != SLOT_EMPTY;
+                const uint64_t v0 = ((j0 + (bj.x & 0xFFFFu)) << 32) | st.x;
+                const uint64_t v1 = ((j0 + (bj.y & 0xFFFFu)) << 32) | st.y;
+                const uint2 ql = qq[d];   // (qs, qlim): both even
+                if (P.ablate & 16) continue;   // timing only: no run writes
+                const uint64_t o = dl[2 * d + (q >= ql.x ? 1 : 0)] + q;
+                if (q < ql.y) {
+                    if (r0 && r1) *(ulonglong2 *)(rec + o) = make_ulonglong2(v0, v1);
+                    else if (r0) rec[o] = v0;
+                    else if (r1) rec[o + 1] = v1;
+                } else if (r0) {
+                    tail[d] = v0;   // the run's unpaired last record
+                }
             }
-            else tail[d] = v;   // the odd last record of the run (not on the last tile)
         }
         if (TW && !last && threadIdx.x < L1F_TW) s_tw[((ti + 1) & 1) * L1F_TW + threadIdx.x] = tw_next;
         block_sync();
