@@ -295,7 +295,7 @@ static uint32_t l1f_workgroups(const Graph *g, uint64_t nkmers) {
 }
 static size_t lds_own_l1f(const Params &P) {
     const size_t F1a = (P.F1 + 3) & ~3u;
-    return (size_t)2 * OWN_BATCH * 8 + F1a * 60 + (size_t)OWN_BATCH * 2 + 48 * 4;
+    return (size_t)OWNF_BUF * 8 + F1a * 60 + (size_t)OWN_BATCH * 2 + 48 * 4 + 2 * L1F_TW * 8;
 }
 // a shard's level 1 in one kernel (k_own_l1f) for fixed-length reads;
 // KH_OWN_L1F=0 falls back to k_own_filter + k_scatter_l1<PRE> (development)
@@ -304,7 +304,17 @@ template <class Src>
 using OwnL1FFn = void (*)(Params, Src, uint64_t, uint64_t, int, int, const uint64_t *, unsigned long long *,
                           uint64_t *, uint64_t *, int);
 template <class Src>
-static OwnL1FFn<Src> own_l1f_kernel(int kpt) {
+static OwnL1FFn<Src> own_l1f_kernel(int kpt, bool tw) {
+    if constexpr (std::is_same<Src, SrcTwoBit>::value) {
+        if (tw) {
+            switch (kpt) {
+                case 1: return k_own_l1f<Src, 1, true>;
+                case 2: return k_own_l1f<Src, 2, true>;
+                case 4: return k_own_l1f<Src, 4, true>;
+                default: return k_own_l1f<Src, 8, true>;
+            }
+        }
+    }
     switch (kpt) {
         case 1: return k_own_l1f<Src, 1>;
         case 2: return k_own_l1f<Src, 2>;
@@ -709,7 +719,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                 while (kpt * 2 * nt <= 8) kpt *= 2;
                 const uint64_t tk = (uint64_t)L1_THREADS * kpt;
                 const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
-                TIMED("own_l1f", hipLaunchKernelGGL(own_l1f_kernel<Src>(kpt), dim3(nwg), dim3(L1_THREADS),
+                TIMED("own_l1f", hipLaunchKernelGGL(own_l1f_kernel<Src>(kpt, l1f_tw(src, kpt)), dim3(nwg), dim3(L1_THREADS),
                                                     lds_own_l1f(P), st, P, src, nkmers, kpw, t0, nt, w.bkt_base,
                                                     (unsigned long long *)w.bkt_cur, w.rec1, w.ctr, l1f_blk_sh()));
             }
@@ -1402,9 +1412,10 @@ static void set_lds_limits() {
         }
     KH_LDS_MAX((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>));
     for (int kpt : {1, 2, 4, 8}) {
-        KH_LDS_MAX(own_l1f_kernel<SrcTwoBit>(kpt));
-        KH_LDS_MAX(own_l1f_kernel<SrcBytes>(kpt));
-        KH_LDS_MAX(own_l1f_kernel<SrcHashes>(kpt));
+        KH_LDS_MAX(own_l1f_kernel<SrcTwoBit>(kpt, false));
+        KH_LDS_MAX(own_l1f_kernel<SrcTwoBit>(kpt, true));
+        KH_LDS_MAX(own_l1f_kernel<SrcBytes>(kpt, false));
+        KH_LDS_MAX(own_l1f_kernel<SrcHashes>(kpt, false));
     }
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 1>));
     KH_LDS_MAX((k_own_filter<SrcTwoBit, 2>));

@@ -774,7 +774,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_filter(Params P, Src src, ui
 #pragma unroll
             for (int i = 0; i < TPK; i++) {
                 uint64_t G;
-                if (i < nt && j < j1 && local_bin(P, t0 + i, hh[a], &G)) {
+                if (i < nt && j < j1 && !(P.ablate & 128) && local_bin(P, t0 + i, hh[a], &G)) {
                     v[a * TPK + i] = (j << 32) | G;
                     own |= 1u << (a * TPK + i);
                 }
@@ -819,23 +819,26 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_filter(Params P, Src src, ui
 // exactly as in k_scatter_l1f (2-record tails, one returning atomic per
 // (bucket, batch, new block)).  The owned records never make the round trip
 // through HBM that k_own_filter + k_hist_rec + k_scatter_l1<PRE> take.
-constexpr int OWN_BATCH = L1_THREADS * 8;   // records sorted per batch
-template <class Src, int KPT>
+// records sorted per batch: 2048 keeps the kernel at ~68 KB of LDS at
+// F1 = 240 (an 8-way shard), two workgroups per CU (4096: one)
+constexpr int OWN_BATCH = L1_THREADS * 4;
+constexpr int OWN_FSLOTS = 8;                                  // candidate records per thread per filter tile
+constexpr int OWNF_BUF = OWN_BATCH + L1_THREADS * OWN_FSLOTS;  // < OWN_BATCH left + one filter tile
+template <class Src, int KPT, bool TW_ = false>
 __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint64_t nkmers, uint64_t kpw, int t0,
                                                        int nt, const uint64_t *bkt_base, unsigned long long *bkt_cur,
                                                        uint64_t *rec, uint64_t *ctr, int blk_sh) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int RPT = 8;
-    constexpr int FSLOTS = 8;                          // candidate records per thread per filter tile
+    constexpr int RPT = OWN_BATCH / L1_THREADS;
+    constexpr int FSLOTS = OWN_FSLOTS;
     constexpr int TPK = FSLOTS / KPT;                  // table slots per k-mer
     constexpr int TILE_KMERS = L1_THREADS * KPT;
-    static_assert(L1_THREADS * FSLOTS <= OWN_BATCH, "a filter tile must fit the buffer's second half");
     const uint32_t BLK = 1u << blk_sh;
     constexpr uint64_t DEAD = ~0ull;
     const uint32_t F1 = P.F1;
     const uint32_t F1a = (F1 + 3) & ~3u;
-    uint64_t *buf = (uint64_t *)smem;                  // [2 * OWN_BATCH] owned records; [0, OWN_BATCH) is the stage while sorting
-    uint64_t *bcur = buf + 2 * OWN_BATCH;              // [F1] partially filled block (DEAD: overflowed)
+    uint64_t *buf = (uint64_t *)smem;                  // [OWNF_BUF] owned records; a batch is its own stage while sorted
+    uint64_t *bcur = buf + OWNF_BUF;                   // [F1] partially filled block (DEAD: overflowed)
     uint64_t *nbase = bcur + F1a;                      // [F1] blocks reserved for this batch
     uint64_t *dl = nbase + F1a;                        // [F1][2] output - LDS position: current block, new blocks
     uint64_t *tail = dl + 2 * F1a;                     // [F1] a pending odd record
@@ -845,6 +848,10 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
     uint2 *qq = (uint2 *)(lstart + F1a);               // [F1] (first LDS position in the new blocks, first left for the tail)
     uint16_t *sb = (uint16_t *)(qq + F1a);             // [OWN_BATCH] bucket of each stage slot
     uint32_t *s_wtot = (uint32_t *)(sb + OWN_BATCH);   // [3][16]: filter scans (tile parity), batch scan
+    // TW: the filter tile's packed words staged in LDS as in k_scatter_l1f
+    // (the next tile's words loaded one tile ahead, one word per thread)
+    constexpr bool TW = TW_ && std::is_same<Src, SrcTwoBit>::value;
+    uint64_t *s_tw = (uint64_t *)(s_wtot + 48);        // [2][L1F_TW] (8-B aligned: F1a and OWN_BATCH are)
     const int shift = P.s0 + P.s2;
     const uint64_t omask = (1ull << shift) - 1;
     for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) {
@@ -854,17 +861,34 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
     }
     const uint64_t c0 = min(nkmers, (uint64_t)blockIdx.x * kpw);
     const uint64_t c1 = min(nkmers, c0 + kpw);
-    typename Src::Pend pend[KPT];
+    constexpr int NPEND = TW ? 1 : KPT;
+    typename Src::Pend pend[NPEND];
+    if (!TW) {
 #pragma unroll
-    for (int a = 0; a < KPT; a++) {
-        const uint64_t j = c0 + (uint64_t)a * L1_THREADS + threadIdx.x;
-        if (j < min(c1, c0 + TILE_KMERS)) pend[a] = kmer_fetch(src, j);
+        for (int a = 0; a < NPEND; a++) {
+            const uint64_t j = c0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            if (j < min(c1, c0 + TILE_KMERS)) pend[a] = kmer_fetch(src, j);
+        }
+    }
+    auto tile_w0 = [&](uint64_t j0) -> uint64_t {
+        const uint64_t ja = j0 + src.kbase;
+        return ((ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2) >> 6;
+    };
+    auto tile_nw = [&](uint64_t j0, uint64_t j1) -> uint32_t { return (uint32_t)(tile_w0(j1 - 1) + 2 - tile_w0(j0)); };
+    uint64_t tw_next = 0;
+    if constexpr (TW) {
+        if (c1 > c0) {
+            const uint64_t e = min(c1, c0 + TILE_KMERS);
+            if (threadIdx.x < tile_nw(c0, e)) s_tw[threadIdx.x] = src.words[tile_w0(c0) + threadIdx.x];
+        }
+        block_sync();
     }
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t nwaves = blockDim.x >> 6;
 
-    // sort buf[0, n) by bucket and append it (last: flush every pending tail)
-    auto sort_batch = [&](uint32_t n, bool last) {
+    // sort buf[o, o + n) by bucket and append it (last: flush every pending tail)
+    auto sort_batch = [&](uint32_t o, uint32_t n, bool last) {
+        uint64_t *bb = buf + o;
         uint32_t off[RPT], br[RPT], jv[RPT];
 #pragma unroll
         for (int u = 0; u < RPT; u++) {
@@ -873,14 +897,14 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
             br[u] = 0;
             jv[u] = 0;
             if (q < n) {
-                const uint64_t x = buf[q];
+                const uint64_t x = bb[q];
                 const uint32_t G = (uint32_t)x, b = G >> shift;
                 off[u] = G & (uint32_t)omask;
                 jv[u] = (uint32_t)(x >> 32);
                 br[u] = (b << 13) | atomicAdd(&hist[b], 1u);
             }
         }
-        block_sync();   // every record is in registers: buf[0, OWN_BATCH) becomes the stage
+        block_sync();   // every record is in registers: bb[0, n) becomes the stage
         block_scan_hist(hist, lstart, F1, s_wtot + 32);
         block_sync();
 #pragma unroll
@@ -888,7 +912,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
             if (off[u] != ~0u) {
                 const uint32_t b = br[u] >> 13;
                 const uint32_t pos = lstart[b] + (br[u] & 8191u);
-                buf[pos] = ((uint64_t)jv[u] << 32) | off[u];
+                bb[pos] = ((uint64_t)jv[u] << 32) | off[u];
                 sb[pos] = (uint16_t)b;
             }
         }
@@ -923,7 +947,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
             const uint32_t q = threadIdx.x + (uint32_t)u * L1_THREADS;
             if (q >= n) continue;
             const uint32_t d = sb[q];
-            const uint64_t v = buf[q];
+            const uint64_t v = bb[q];
             const uint2 ql = qq[d];
             if (q < ql.y) rec[dl[2 * d + (q >= ql.x ? 1 : 0)] + q] = v;
             else tail[d] = v;   // the odd last record of the run (not on the last batch)
@@ -951,15 +975,34 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
         uint64_t v[FSLOTS];
         uint32_t own = 0;   // bit q: record slot q is owned here
         uint64_t hh[KPT];
-#pragma unroll
-        for (int a = 0; a < KPT; a++) {
-            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
-            hh[a] = j < j1 ? src.finish(pend[a]) : 0;
-        }
-        {
-            const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
+        const uint64_t *tw_cur = s_tw + (ti & 1) * L1F_TW;
+        if constexpr (TW) {
+            const uint64_t tw_w0 = tile_w0(j0);
 #pragma unroll
             for (int a = 0; a < KPT; a++) {
+                const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+                uint64_t h = 0;
+                if (j < j1) {
+                    const uint64_t ja = j + src.kbase;
+                    const uint64_t bpos = (ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2;
+                    const uint32_t wi = (uint32_t)((bpos >> 6) - tw_w0);
+                    h = src.finish(SrcTwoBit::Pend{tw_cur[wi], tw_cur[wi + 1], (uint32_t)(bpos & 63)});
+                }
+                hh[a] = h;
+            }
+            if (ti + 1 < ntiles) {   // the next tile's words (stored after this tile's scan barrier)
+                const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
+                if (threadIdx.x < tile_nw(n0, n1)) tw_next = src.words[tile_w0(n0) + threadIdx.x];
+            }
+        } else {
+#pragma unroll
+            for (int a = 0; a < KPT; a++) {
+                const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+                hh[a] = j < j1 ? src.finish(pend[a]) : 0;
+            }
+            const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
+#pragma unroll
+            for (int a = 0; a < NPEND; a++) {
                 const uint64_t j = n0 + (uint64_t)a * L1_THREADS + threadIdx.x;
                 if (j < n1) pend[a] = kmer_fetch(src, j);
             }
@@ -970,7 +1013,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
 #pragma unroll
             for (int i = 0; i < TPK; i++) {
                 uint64_t G;
-                if (i < nt && j < j1 && local_bin(P, t0 + i, hh[a], &G)) {
+                if (i < nt && j < j1 && !(P.ablate & 128) && local_bin(P, t0 + i, hh[a], &G)) {
                     v[a * TPK + i] = (j << 32) | G;
                     own |= 1u << (a * TPK + i);
                 }
@@ -998,15 +1041,22 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
         for (int q = 0; q < FSLOTS; q++)
             if ((own >> q) & 1) buf[pos + __builtin_popcount(own & ((1u << q) - 1))] = v[q];
         nbuf += tot;
+        if (P.ablate & 64) nbuf = 0;   // timing only: the filter without the bucket placement
+        // buffer (ti + 1) & 1 was last read in tile ti - 1, before this tile's scan barrier
+        if (TW && ti + 1 < ntiles && threadIdx.x < L1F_TW) s_tw[((ti + 1) & 1) * L1F_TW + threadIdx.x] = tw_next;
         block_sync();
         const bool lt = ti + 1 == ntiles;
-        while (nbuf >= (uint32_t)OWN_BATCH || (lt && !flushed_last)) {
-            const uint32_t n = min(nbuf, (uint32_t)OWN_BATCH);
-            const bool last = lt && nbuf == n;
-            sort_batch(n, last);
+        uint32_t o = 0;   // batches buf[o, o + OWN_BATCH) in order; the rest (< OWN_BATCH) moves to the front
+        while (nbuf - o >= (uint32_t)OWN_BATCH || (lt && !flushed_last)) {
+            const uint32_t n = min(nbuf - o, (uint32_t)OWN_BATCH);
+            const bool last = lt && nbuf - o == n;
+            sort_batch(o, n, last);
             flushed_last = last;
-            for (uint32_t x = threadIdx.x; x < nbuf - n; x += blockDim.x) buf[x] = buf[n + x];   // leftover to the front
-            nbuf -= n;
+            o += n;
+        }
+        if (o) {   // the rest is shorter than o: source and destination do not overlap
+            for (uint32_t x = threadIdx.x; x < nbuf - o; x += blockDim.x) buf[x] = buf[o + x];
+            nbuf -= o;
             block_sync();
         }
     }
