@@ -98,6 +98,37 @@ def parse():
     return a
 
 
+FIXTURE_GRAPH = {(1, 0): "Countgraph", (2, 0): "Nodegraph", (7, 0): "SmallCountgraph", (7, 1): "SmallCounttable"}
+
+
+def matching_fixture(args, total_reads):
+    """The oracle golden fixture (tests/golden/full/*.json, made by
+    tests/golden/make_full_fixtures.py) whose workload is exactly this run's
+    whole stream, if any: then the bench line carries a parity check of its
+    own (counters and per-table SHA-256 against the single-threaded oracle)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "full", "*.json"))):
+        try:
+            with open(path) as fh:
+                fx = json.load(fh)
+            p = fx["params"]
+        except (OSError, ValueError, KeyError):
+            continue
+        if (FIXTURE_GRAPH.get((p["kind"], p["hash"])) == args.graph and p["k"] == args.k and p["n"] == args.tables
+                and float(p["x"]) == float(args.x) and p["reads"] == total_reads and p["L"] == args.read_len
+                and bool(p["bigcount"]) == bool(args.bigcount) and int(p["genome"]) == int(args.genome)):
+            return fx
+    return None
+
+
+def compare_fixture(fx, n_unique, n_occupied, table_sha):
+    out = {"fixture": fx["config"], "counters_match": n_unique == fx["n_unique_kmers"] and
+           n_occupied == fx["n_occupied"]}
+    if table_sha is not None:
+        out["tables_match"] = list(table_sha) == list(fx["table_sha256"])
+    return out
+
+
 def kernel_stats(lib, g):
     buf = ctypes.create_string_buffer(1 << 16)
     n = ctypes.c_size_t()
@@ -224,10 +255,52 @@ def cpu_baseline(args, sizes):
     }
 
 
+def free_port():
+    import socket
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N rank processes of
+    this script (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+    MASTER_PORT set as torchrun would), before this process makes any HIP
+    call.  Rank 0's JSON line is the output; any failing rank fails the run
+    (the others are stopped)."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                sys.stderr.write("bench.py: rank %d exited with %d; stopping the others\n" % (procs.index(p), code))
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 1
+
+
 def main():
     args = parse()
     if args.ablate:
         os.environ["KH_ABLATE"] = str(args.ablate)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -272,6 +345,12 @@ def main():
     stats = runner.kernel_stats()
     runner.profile(False)
     check_info = runner.check()
+    # parity of the timed workload itself, when a golden fixture holds it
+    fx = None if args.query else matching_fixture(args, nreads * world)
+    if fx is not None:
+        sha = runner.table_sha256()   # collective when sharded
+        if rank == 0:
+            check_info.update(compare_fixture(fx, check_info["n_unique_kmers"], check_info["n_occupied"], sha))
 
     bpk = query_bytes_per_kmer(L, k, nt) if args.query else algorithmic_bytes_per_kmer(L, k, nt)
     total_kmers = nkmers * world * args.steps
@@ -429,10 +508,21 @@ class SingleGpuBench(object):
     def kernel_stats(self):
         return kernel_stats(self.lib, self.g._g)
 
+    def table_sha256(self):
+        import hashlib
+        out = []
+        for i, n in enumerate(self.g._raw_sizes()):
+            buf = bytearray(n)
+            self._ck(self.lib.kh_graph_copy_table(self.g._g, i, (ctypes.c_char * n).from_buffer(buf)))
+            out.append(hashlib.sha256(buf).hexdigest())
+            del buf
+        return out
+
     def check(self):
         """Counters of the last consume (the full workload into empty tables);
         --query: also a checksum of the medians."""
         out = {"n_unique_kmers": self.g.n_unique_kmers(), "n_occupied": self.g.n_occupied()}
+
         if self.args.query:
             import hashlib
             n = self.args.reads

@@ -143,7 +143,12 @@ int kh_consume_packed_device(kh_graph *g, const uint64_t *d_words, const uint64_
 int kh_consume_packed_fixed_device(kh_graph *g, const uint64_t *d_words, uint64_t nreads, uint32_t read_len);
 /* Murmur graphs (Counttable family, include/oxli/hashtable.hh:494-627): ASCII
  * reads of one length already in device memory, read r at byte r*read_len;
- * MurmurKmerHashIterator over each (src/oxli/kmer_hash.cc:177-198). */
+ * MurmurKmerHashIterator over each (src/oxli/kmer_hash.cc:177-198).
+ * The kernels read every k-mer as aligned 8-byte words, up to 64 bytes past
+ * the last read: when the allocation holding d_bytes ends less than 64 bytes
+ * after nreads*read_len, the library first copies the reads into a padded
+ * buffer of its own (correct for any buffer; allocate +64 bytes to avoid the
+ * copy). */
 int kh_consume_bytes_fixed_device(kh_graph *g, const uint8_t *d_bytes, uint64_t nreads, uint32_t read_len);
 /* explicit hashes: Hashtable::count/add(HashIntoType) (include/oxli/hashtable.hh:222-243);
  * is_new[n] (nullable) receives Storage::add's return per hash, in order. */
@@ -158,10 +163,28 @@ int kh_median_counts(kh_graph *g, const char *seqs, const uint64_t *offsets, uin
                      uint16_t *med, float *avg, float *stddev, uint8_t *status);
 /* get_median_count per read of device-resident fixed-length reads (2-bit
  * packed words for 2-bit graphs, ASCII bytes for Murmur graphs), outputs in
- * device memory; read_len - k + 1 <= 256.  Same values as kh_median_counts
+ * device memory; read_len - k + 1 <= 256.  ASCII input: the padding rule of
+ * kh_consume_bytes_fixed_device applies (2-bit input: the packed layout's
+ * trailing word, as kh_synth_packed_device writes it).  Same values as kh_median_counts
  * (src/oxli/hashtable.cc:299-328; scripts/count-median.py:123 is the caller). */
 int kh_median_counts_fixed_device(kh_graph *g, const void *d_reads, uint64_t nreads, uint32_t read_len,
                                   uint16_t *d_med, float *d_avg, float *d_stddev);
+/* Hashtable::get_kmer_hashes / get_kmer_counts (src/oxli/hashtable.cc:378-388,
+ * 403-413) over a batch of reads (raw, no cleaning: the table's own k-mer
+ * iterator), on the device.  Reads shorter than k contribute nothing; out
+ * receives the k-mers of the remaining reads back to back (*n_out of them;
+ * out must hold sum(len - k + 1) entries). */
+int kh_graph_kmer_hashes(kh_graph *g, const char *seqs, const uint64_t *offsets, uint64_t nreads,
+                         uint64_t *out, uint64_t *n_out);
+int kh_graph_kmer_counts(kh_graph *g, const char *seqs, const uint64_t *offsets, uint64_t nreads,
+                         uint16_t *out, uint64_t *n_out);
+/* Hashtable::median_at_least per read (src/oxli/hashtable.cc:333-364; the
+ * normalize-by-median filter, khmer/trimming.py:45): out[r] = 1 when at least
+ * unsigned(0.5 + float(n)/2) of the read's n k-mers have a count >= cutoff.
+ * Reads shorter than k get status[r] = 1 and out[r] = 0 (the reference's
+ * Python binding raises ValueError for them, graphs.pyx:182-185). */
+int kh_median_at_least(kh_graph *g, const char *seqs, const uint64_t *offsets, uint64_t nreads, uint32_t cutoff,
+                       uint8_t *out, uint8_t *status);
 /* Hashtable::abundance_distribution (src/oxli/hashtable.cc:451-493);
  * dist[65536]. */
 int kh_abundance_distribution(kh_graph *g, kh_parser *p, kh_graph *tracking, uint64_t *dist);
@@ -182,7 +205,8 @@ int kh_graph_load(const char *path, int expected_storage, int hash_kind, int dev
  * out[7] = {version, type, use_bigcount (-1 when absent), k, n_tables,
  * n_occupied, first table size}.  KH_EFILE when the file is short or does not
  * start with "OXLI". */
-int kh_file_header(const char *path, int layout, int64_t *out);int kh_graph_n_tags(kh_graph *g, uint64_t *out);
+int kh_file_header(const char *path, int layout, int64_t *out);
+int kh_graph_n_tags(kh_graph *g, uint64_t *out);
 int kh_graph_get_tags(kh_graph *g, uint64_t *out);              /* ascending */
 int kh_graph_add_tag(kh_graph *g, uint64_t h);
 int kh_graph_save_tagset(kh_graph *g, const char *path);        /* hashgraph.cc:55-88 */

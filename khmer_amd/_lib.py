@@ -78,6 +78,10 @@ SIGNATURES = {
     "kh_median_counts": (i32, [P, ctypes.c_char_p, PU64, u64, ctypes.POINTER(ctypes.c_uint16),
                                ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                ctypes.POINTER(ctypes.c_uint8)]),
+    "kh_graph_kmer_hashes": (i32, [P, ctypes.c_char_p, PU64, u64, PU64, PU64]),
+    "kh_graph_kmer_counts": (i32, [P, ctypes.c_char_p, PU64, u64, ctypes.POINTER(ctypes.c_uint16), PU64]),
+    "kh_median_at_least": (i32, [P, ctypes.c_char_p, PU64, u64, u32, ctypes.POINTER(ctypes.c_uint8),
+                                 ctypes.POINTER(ctypes.c_uint8)]),
     "kh_abundance_distribution": (i32, [P, P, P, PU64]),
     "kh_graph_table_nbytes": (i32, [P, i32, PU64]),
     "kh_graph_copy_table": (i32, [P, i32, ctypes.c_void_p]),

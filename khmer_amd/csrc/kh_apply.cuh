@@ -176,13 +176,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
     Prefetch cur, nxt;
     prefetch_region<KIND, TH>(P, A, blockIdx.x, total, load_bounds(P, A, blockIdx.x, total), cur);
     Bounds bnext = load_bounds(P, A, blockIdx.x + gridDim.x, total);
-#ifdef KH_PHASES
-    uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t tA = __builtin_amdgcn_s_memtime(), tB;
-#define PH(i) do { tB = __builtin_amdgcn_s_memtime(); ph[i] += tB - tA; tA = tB; } while (0)
-#else
-#define PH(i) do { } while (0)
-#endif
+    PH_BEGIN(6);
     for (uint64_t rr = blockIdx.x; rr < total; rr += gridDim.x) {
         const RegionInfo ri = cur.ri;
         if (ri.e0 == ri.e1) {
@@ -387,11 +381,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
         PH(3);
         cur = nxt;
     }
-#ifdef KH_PHASES
-    if (threadIdx.x == 0)
-        for (int z = 0; z < 6; z++) atomicAdd(&g_dbg[16 + z], (unsigned long long)ph[z]);
-#endif
-#undef PH
+    PH_END(16, 6);
     occ = wave_sum(occ);
     if ((threadIdx.x & 63) == 0 && occ) atomicAdd((unsigned long long *)&A.ctr[CTR_OCC], (unsigned long long)occ);
 }

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <fstream>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <condition_variable>
 #include <deque>
@@ -36,11 +37,10 @@ struct PlainFile;
 PlainFile *parser_plain_open(Parser *pr);
 void parser_plain_close(PlainFile *f);
 size_t plain_size(const PlainFile *f);
-size_t plain_record_start(const PlainFile *f, size_t from);
+size_t plain_record_start(const PlainFile *f, size_t from, size_t limit);
 uint64_t plain_parse_range(const PlainFile *f, size_t start, size_t stop, int k, uint64_t max_kmers,
                            std::vector<RawBatch> &out, uint64_t *nreads);
 void parser_mark_drained(Parser *pr, uint64_t nreads);
-void engine_hash_batch(Graph *g, const HostBatch &b, uint64_t *h_out);
 void engine_synth_packed(int device, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L, int k,
                          uint64_t *d_words, uint64_t *d_koff);
 }  // namespace kh
@@ -331,7 +331,7 @@ static void pack_raw(const RawBatch &raw, HostBatch &b, int k, int hash) {
 // starts where the previous one really ended (otherwise it parses the rest
 // of the file itself, serially).  Same reads, same order, same errors as the
 // serial parser.
-static void consume_chunked(Graph *g, Parser *parser, PlainFile *pf, uint64_t *nreads_out, uint64_t *consumed) {
+static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, uint64_t *nreads_out, uint64_t *consumed) {
     struct Chunk {
         std::vector<RawBatch> raw;
         std::vector<HostBatch> packed;
@@ -343,6 +343,9 @@ static void consume_chunked(Graph *g, Parser *parser, PlainFile *pf, uint64_t *n
     const char *ce = getenv("KH_FEED_CHUNK");   // development / tests: chunk bytes
     const size_t CH = ce && atoll(ce) > 0 ? (size_t)atoll(ce) : (size_t)64 << 20;
     const size_t nch = (n + CH - 1) / CH;
+    // no recognisable record start inside the second chunk (CRLF or wrapped
+    // FASTQ): the streaming reader/packer pipeline instead
+    if (nch > 1 && plain_record_start(pf, CH, CH) >= n) return false;
     const int T = std::max(1, feed_threads() - 1);
     const size_t depth = (size_t)T * 2;
     const uint64_t maxk = std::min<uint64_t>(g->batch_kmers, 1ull << 27);
@@ -366,8 +369,16 @@ static void consume_chunked(Graph *g, Parser *parser, PlainFile *pf, uint64_t *n
                 }
                 Chunk &C = *ch[c];
                 try {
-                    C.start = plain_record_start(pf, c * CH);
-                    const size_t stop_at = c + 1 < nch ? plain_record_start(pf, (c + 1) * CH) : n;
+                    // a chunk without a recognised record start parses nothing
+                    // (the consumer then continues serially); a chunk whose
+                    // successor has none stops at the first record boundary
+                    // past its own end, so no chunk holds much more than CH
+                    C.start = plain_record_start(pf, c * CH, CH);
+                    size_t stop_at = n;
+                    if (c + 1 < nch) {
+                        stop_at = plain_record_start(pf, (c + 1) * CH, CH);
+                        if (stop_at >= n) stop_at = (c + 1) * CH;
+                    }
                     C.end = C.start < n ? plain_parse_range(pf, C.start, stop_at, k, maxk, C.raw, &C.nreads) : n;
                 } catch (...) {
                     C.err = std::current_exception();
@@ -428,12 +439,15 @@ static void consume_chunked(Graph *g, Parser *parser, PlainFile *pf, uint64_t *n
         throw;
     }
     finish();
-    if (serial_rest && true_end < n) {
+    // the rest of the file serially, in pieces of about CH bytes (each piece
+    // ends on a real record boundary), so host memory stays bounded
+    while (serial_rest && true_end < n) {
         std::vector<RawBatch> raw;
         uint64_t nr = 0;
         std::exception_ptr err;
+        size_t end = n;
         try {
-            plain_parse_range(pf, true_end, n, k, maxk, raw, &nr);
+            end = plain_parse_range(pf, true_end, std::min(n, true_end + CH), k, maxk, raw, &nr);
         } catch (...) {
             err = std::current_exception();
         }
@@ -449,16 +463,18 @@ static void consume_chunked(Graph *g, Parser *parser, PlainFile *pf, uint64_t *n
             parser_mark_drained(parser, total);
             std::rethrow_exception(err);
         }
+        if (end <= true_end) break;   // no progress: end of input
+        true_end = end;
     }
     *nreads_out = total;
     parser_mark_drained(parser, total);
+    return true;
 }
 
 static void consume_pipelined(Graph *g, Parser *parser, uint64_t *nreads_out, uint64_t *consumed) {
     if (PlainFile *pf = parser_plain_open(parser)) {
         std::unique_ptr<PlainFile, void (*)(PlainFile *)> hold(pf, parser_plain_close);
-        consume_chunked(g, parser, pf, nreads_out, consumed);
-        return;
+        if (consume_chunked(g, parser, pf, nreads_out, consumed)) return;
     }
     const int T = feed_threads();
     const int npack = std::max(1, T - 1);
@@ -638,9 +654,16 @@ int kh_consume_parser_filtered(kh_graph *h, kh_parser *ph, uint32_t num_bands, u
             f.threshold = threshold;
             f.consume_masked = consume_masked;
         }
-        std::lock_guard<std::recursive_mutex> lk(g->mu);
-        std::unique_ptr<std::lock_guard<std::recursive_mutex>> mlk;
-        if (f.mask) mlk.reset(new std::lock_guard<std::recursive_mutex>(f.mask->mu));
+        // table and mask locked together (no lock-order inversion between
+        // two threads filtering each table by the other)
+        std::unique_lock<std::recursive_mutex> lk(g->mu, std::defer_lock);
+        std::unique_lock<std::recursive_mutex> mlk;
+        if (f.mask) {
+            mlk = std::unique_lock<std::recursive_mutex>(f.mask->mu, std::defer_lock);
+            std::lock(lk, mlk);
+        } else {
+            lk.lock();
+        }
         KH_HIP(hipSetDevice(g->device));
         HostBatch b;
         b.hash = g->hash;
@@ -793,14 +816,82 @@ int kh_median_counts(kh_graph *h, const char *seqs, const uint64_t *offsets, uin
     });
 }
 
+// a batch of raw (uncleaned) reads of >= k bases; the others get status 1
+static void raw_batch(Graph *g, const char *seqs, const uint64_t *offsets, uint64_t nreads, HostBatch &b,
+                      std::vector<uint64_t> &idx, uint8_t *status) {
+    b.hash = g->hash;
+    for (uint64_t r = 0; r < nreads; r++) {
+        const char *s = seqs + offsets[r];
+        const size_t len = strnlen(s, (size_t)(offsets[r + 1] - offsets[r]));
+        const bool ok = len >= (size_t)g->k;
+        if (ok) {
+            b.append(s, len, g->k, false);
+            idx.push_back(r);
+        }
+        if (status) status[r] = ok ? 0 : 1;
+    }
+}
+
+int kh_graph_kmer_hashes(kh_graph *h, const char *seqs, const uint64_t *offsets, uint64_t nreads, uint64_t *out,
+                         uint64_t *n_out) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        HostBatch b;
+        std::vector<uint64_t> idx;
+        raw_batch(g, seqs, offsets, nreads, b, idx, nullptr);
+        *n_out = b.nkmers();
+        if (b.nkmers()) engine_hash_batch(g, b, out);
+    });
+}
+
+int kh_graph_kmer_counts(kh_graph *h, const char *seqs, const uint64_t *offsets, uint64_t nreads, uint16_t *out,
+                         uint64_t *n_out) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        HostBatch b;
+        std::vector<uint64_t> idx;
+        raw_batch(g, seqs, offsets, nreads, b, idx, nullptr);
+        *n_out = b.nkmers();
+        if (b.nkmers()) engine_kmer_counts(g, b, out);
+    });
+}
+
+int kh_median_at_least(kh_graph *h, const char *seqs, const uint64_t *offsets, uint64_t nreads, uint32_t cutoff,
+                       uint8_t *out, uint8_t *status) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        KH_HIP(hipSetDevice(g->device));
+        HostBatch b;
+        std::vector<uint64_t> idx;
+        raw_batch(g, seqs, offsets, nreads, b, idx, status);
+        for (uint64_t r = 0; r < nreads; r++) out[r] = 0;
+        if (!b.nreads()) return;
+        std::vector<uint8_t> res(b.nreads());
+        engine_median_at_least(g, b, cutoff, res.data());
+        for (size_t t = 0; t < idx.size(); t++) out[idx[t]] = res[t];
+    });
+}
+
 int kh_abundance_distribution(kh_graph *h, kh_parser *ph, kh_graph *th, uint64_t *dist) {
     return guard([&] {
         CHECK_PTR(h);
         CHECK_PTR(ph);
         CHECK_PTR(th);
         Graph *g = h->g, *t = th->g;
-        std::lock_guard<std::recursive_mutex> lk(g->mu);
-        std::lock_guard<std::recursive_mutex> lk2(t->mu);
+        // both tables locked together (std::lock's deadlock avoidance): two
+        // threads calling a.abundance_distribution(.., b) and
+        // b.abundance_distribution(.., a) must not take them in opposite order
+        std::unique_lock<std::recursive_mutex> lk(g->mu, std::defer_lock), lk2(t->mu, std::defer_lock);
+        if (g == t) lk.lock();
+        else std::lock(lk, lk2);
         KH_HIP(hipSetDevice(g->device));
         if (t->device != g->device) fail(KH_EVALUE, "tracking table must live on the same device");
         memset(dist, 0, 65536 * sizeof(uint64_t));

@@ -1223,6 +1223,56 @@ void engine_get_counts(Graph *g, const uint64_t *h_hashes, uint64_t n, uint16_t 
     KH_HIP(hipStreamSynchronize(g->stream));
 }
 
+// per-k-mer counts of an uploaded host batch into d_counts (device)
+static void batch_counts(Graph *g, const HostBatch &b, uint16_t *d_counts) {
+    const uint64_t nk = b.nkmers(), nr = b.nreads();
+    const uint64_t tiles = (nk + Q_TILE - 1) / Q_TILE;
+    const size_t lds = 16 + (Q_TILE + 2) * 8;
+    if (!tiles) return;
+    if (b.hash == MURMUR) {
+        SrcBytes s = src_bytes_host(g, b);
+        s.koff = g->ws.d_koff;
+        s.nreads = nr;
+        hipLaunchKernelGGL(k_kmer_counts<SrcBytes>, dim3((unsigned)tiles), dim3(Q_THREADS), lds, g->stream, g->prm, s,
+                           nk, g->d_tab, d_counts, g->d_bc_keys, g->d_bc_vals, g->d_bc_n);
+    } else {
+        SrcTwoBit s = src_twobit(g, g->ws.d_words);
+        s.koff = g->ws.d_koff;
+        s.nreads = nr;
+        hipLaunchKernelGGL(k_kmer_counts<SrcTwoBit>, dim3((unsigned)tiles), dim3(Q_THREADS), lds, g->stream, g->prm,
+                           s, nk, g->d_tab, d_counts, g->d_bc_keys, g->d_bc_vals, g->d_bc_n);
+    }
+    KH_HIP(hipGetLastError());
+}
+
+// Hashtable::get_kmer_counts (src/oxli/hashtable.cc:403-413) over a batch
+void engine_kmer_counts(Graph *g, const HostBatch &b, uint16_t *h_out) {
+    const uint64_t nk = b.nkmers();
+    if (!nk) return;
+    engine_sync_bigcounts(g);
+    upload_batch(g, b);
+    DevBuf b_counts(nk * 2 + 64);
+    batch_counts(g, b, b_counts.as<uint16_t>());
+    KH_HIP(hipMemcpyAsync(h_out, b_counts.p, nk * 2, hipMemcpyDeviceToHost, g->stream));
+    KH_HIP(hipStreamSynchronize(g->stream));
+}
+
+// Hashtable::median_at_least (src/oxli/hashtable.cc:333-364) per read of a batch
+void engine_median_at_least(Graph *g, const HostBatch &b, uint32_t cutoff, uint8_t *h_out) {
+    const uint64_t nk = b.nkmers(), nr = b.nreads();
+    if (!nr) return;
+    engine_sync_bigcounts(g);
+    upload_batch(g, b);
+    DevBuf b_counts(nk * 2 + 64), b_out(nr + 64);
+    batch_counts(g, b, b_counts.as<uint16_t>());
+    const unsigned grid = (unsigned)std::min<uint64_t>((nr + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_at_least, dim3(grid), dim3(256), 0, g->stream, g->ws.d_koff, nr, b_counts.as<uint16_t>(),
+                       cutoff, b_out.as<uint8_t>());
+    KH_HIP(hipGetLastError());
+    KH_HIP(hipMemcpyAsync(h_out, b_out.p, nr, hipMemcpyDeviceToHost, g->stream));
+    KH_HIP(hipStreamSynchronize(g->stream));
+}
+
 void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, float *sd) {
     const uint64_t nk = b.nkmers(), nr = b.nreads();
     if (!nr) return;
@@ -1231,23 +1281,7 @@ void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, floa
     DevBuf b_counts(nk * 2 + 64), b_med(nr * 2 + 64), b_avg(nr * 4 + 64), b_sd(nr * 4 + 64);
     uint16_t *d_counts = b_counts.as<uint16_t>(), *d_med = b_med.as<uint16_t>();
     float *d_avg = b_avg.as<float>(), *d_sd = b_sd.as<float>();
-    const uint64_t tiles = (nk + Q_TILE - 1) / Q_TILE;
-    const size_t lds = 16 + (Q_TILE + 2) * 8;
-    if (tiles) {
-        if (b.hash == MURMUR) {
-            SrcBytes s = src_bytes_host(g, b);
-            s.koff = g->ws.d_koff;
-            s.nreads = nr;
-            hipLaunchKernelGGL(k_kmer_counts<SrcBytes>, dim3((unsigned)tiles), dim3(Q_THREADS), lds, g->stream, g->prm,
-                               s, nk, g->d_tab, d_counts, g->d_bc_keys, g->d_bc_vals, g->d_bc_n);
-        } else {
-            SrcTwoBit s = src_twobit(g, g->ws.d_words);
-            s.koff = g->ws.d_koff;
-            s.nreads = nr;
-            hipLaunchKernelGGL(k_kmer_counts<SrcTwoBit>, dim3((unsigned)tiles), dim3(Q_THREADS), lds, g->stream,
-                               g->prm, s, nk, g->d_tab, d_counts, g->d_bc_keys, g->d_bc_vals, g->d_bc_n);
-        }
-    }
+    batch_counts(g, b, d_counts);
     const unsigned grid = (unsigned)std::min<uint64_t>((nr + 255) / 256, 65536);
     hipLaunchKernelGGL(k_median, dim3(grid), dim3(256), 0, g->stream, g->ws.d_koff, nr, d_counts, d_med, d_avg, d_sd);
     KH_HIP(hipGetLastError());
@@ -1255,6 +1289,24 @@ void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, floa
     KH_HIP(hipMemcpyAsync(avg, d_avg, nr * 4, hipMemcpyDeviceToHost, g->stream));
     KH_HIP(hipMemcpyAsync(sd, d_sd, nr * 4, hipMemcpyDeviceToHost, g->stream));
     KH_HIP(hipStreamSynchronize(g->stream));
+}
+
+// Caller-owned ASCII reads are hashed from aligned 8-byte word windows that
+// read up to 64 bytes past the last read (load_window): when the allocation
+// holding them does not extend that far, they are copied into a padded
+// workspace buffer first (include/khmer_hip.h, kh_consume_bytes_fixed_device).
+static const uint8_t *padded_bytes(Graph *g, const uint8_t *d, uint64_t n) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)d) == hipSuccess && base &&
+        (uint64_t)((const uint8_t *)d - (const uint8_t *)base) + n + 64 <= (uint64_t)size)
+        return d;
+    (void)hipGetLastError();
+    Workspace &w = g->ws;
+    ensure((void **)&w.d_bytes, &w.cap_bytes, n + 64, 1);
+    KH_HIP(hipMemcpyAsync(w.d_bytes, d, n, hipMemcpyDeviceToDevice, g->stream));
+    KH_HIP(hipMemsetAsync(w.d_bytes + n, 0, 64, g->stream));
+    return w.d_bytes;
 }
 
 // get_median_count over device-resident fixed-length reads (packed 2-bit words
@@ -1268,7 +1320,8 @@ void engine_median_fixed_device(Graph *g, const void *d_reads, uint64_t nreads, 
     engine_sync_bigcounts(g);
     const unsigned grid = (unsigned)std::min<uint64_t>((nreads + 3) / 4, 8192);
     if (g->hash == MURMUR) {
-        SrcBytes s = src_bytes(g, (const uint8_t *)d_reads, nullptr, nreads, kpr, nreads * read_len);
+        const uint8_t *rd = padded_bytes(g, (const uint8_t *)d_reads, nreads * read_len);
+        SrcBytes s = src_bytes(g, rd, nullptr, nreads, kpr, nreads * read_len);
         set_fixed(s, kpr);
         TIMED("median", hipLaunchKernelGGL(k_median_fixed<SrcBytes>, dim3(grid), dim3(256), 0, g->stream, g->prm, s,
                                            nreads, (uint32_t)kpr, g->d_tab, g->d_bc_keys, g->d_bc_vals, g->d_bc_n,
@@ -1288,6 +1341,7 @@ void engine_median_fixed_device(Graph *g, const void *d_reads, uint64_t nreads, 
 void engine_consume_bytes_fixed(Graph *g, const uint8_t *d_bytes, uint64_t nreads, uint64_t read_len) {
     if (read_len < (uint64_t)g->k) fail(KH_EVALUE, "reads shorter than k");
     const uint64_t kpr = read_len - g->k + 1;
+    d_bytes = padded_bytes(g, d_bytes, nreads * read_len);
     consume_reads(g, src_bytes(g, d_bytes, nullptr, nreads, kpr, nreads * read_len), nullptr, nreads, nreads * kpr, kpr,
                   nullptr);
 }

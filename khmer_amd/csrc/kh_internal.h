@@ -253,6 +253,9 @@ struct BandMask {
 };
 uint64_t engine_consume_filtered(Graph *g, const HostBatch &b, const BandMask &f);
 void engine_median(Graph *g, const HostBatch &b, uint16_t *med, float *avg, float *sd);
+void engine_kmer_counts(Graph *g, const HostBatch &b, uint16_t *h_out);
+void engine_median_at_least(Graph *g, const HostBatch &b, uint32_t cutoff, uint8_t *h_out);
+void engine_hash_batch(Graph *g, const HostBatch &b, uint64_t *h_out);
 void engine_median_fixed_device(Graph *g, const void *d_reads, uint64_t nreads, uint64_t read_len, uint16_t *d_med,
                                 float *d_avg, float *d_sd);
 void engine_consume_bytes_fixed(Graph *g, const uint8_t *d_bytes, uint64_t nreads, uint64_t read_len);

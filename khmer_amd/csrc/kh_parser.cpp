@@ -409,10 +409,14 @@ PlainFile *parser_plain_open(Parser *pr) {
 void parser_plain_close(PlainFile *f) { delete f; }
 size_t plain_size(const PlainFile *f) { return f->n; }
 
-// the first record start at or after `from` (f->n if none)
-size_t plain_record_start(const PlainFile *f, size_t from) {
+// the first record start in [from, from + limit) (f->n if none there): the
+// search is bounded, so a file whose records the heuristic cannot recognise
+// (CRLF or line-wrapped FASTQ) costs each chunk at most `limit` bytes of scan
+size_t plain_record_start(const PlainFile *f, size_t from, size_t limit) {
     const unsigned char *p = f->p, *e = f->p + f->n;
     if (from == 0) return 0;
+    if (from >= f->n) return f->n;
+    const unsigned char *lim = limit < f->n - from ? p + from + limit : e;
     auto line_end = [&](const unsigned char *q) -> const unsigned char * {
         const void *x = memchr(q, '\n', (size_t)(e - q));
         return x ? (const unsigned char *)x : e;
@@ -442,7 +446,7 @@ size_t plain_record_start(const PlainFile *f, size_t from) {
         *next = q1 < e ? q1 + 1 : e;
         return true;
     };
-    while (q < e) {
+    while (q < lim) {
         if (!f->fastq) {
             if (*q == '>') return (size_t)(q - p);
         } else if (*q == '@') {

@@ -23,6 +23,19 @@
 namespace kh {
 __device__ unsigned long long g_dbg[64];   // development phase counters (tools/phase_probe.py)
 
+// Development phase stamps (-DKH_PHASES builds only; tools/phase_probe.py):
+// PH_BEGIN starts the clock, PH(i) adds the cycles since the last stamp to
+// phase i, PH_END(base) publishes a workgroup's totals at g_dbg[base + i].
+#ifdef KH_PHASES
+#define PH_BEGIN(n) uint64_t ph_[n] = {}; uint64_t phA_ = __builtin_amdgcn_s_memtime(), phB_
+#define PH(i) do { phB_ = __builtin_amdgcn_s_memtime(); ph_[i] += phB_ - phA_; phA_ = phB_; } while (0)
+#define PH_END(base, n) do { if (threadIdx.x == 0) for (int z_ = 0; z_ < (n); z_++) atomicAdd(&g_dbg[(base) + z_], (unsigned long long)ph_[z_]); } while (0)
+#else
+#define PH_BEGIN(n) do { } while (0)
+#define PH(i) do { } while (0)
+#define PH_END(base, n) do { } while (0)
+#endif
+
 constexpr int L1_THREADS = 512;
 constexpr int L1_MAX_RPT = 8;                      // records per thread per tile
 constexpr int L1_TILE_RECS = L1_THREADS * L1_MAX_RPT;   // 4096
@@ -315,13 +328,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
     for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) em.init(b, O1[(uint64_t)b * nch1 + blockIdx.x]);
     const uint64_t c0 = (uint64_t)blockIdx.x * ck1;
     const uint64_t c1 = min(nkmers, c0 + ck1);
-#ifdef KH_PHASES
-    uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t tA = __builtin_amdgcn_s_memtime(), tB;
-#define PH(i) do { tB = __builtin_amdgcn_s_memtime(); ph[i] += tB - tA; tA = tB; } while (0)
-#else
-#define PH(i) do { } while (0)
-#endif
+    PH_BEGIN(6);
     // Without a read-offset window the next tile's input words are loaded a
     // whole tile ahead (fetch) and hashed at the top of the tile (finish):
     // the loads are issued before this tile's stores (loads and stores share
@@ -413,11 +420,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
         PH(4);
         em.advance(F1, last);
     }
-#ifdef KH_PHASES
-    if (threadIdx.x == 0)
-        for (int z = 0; z < 6; z++) atomicAdd(&g_dbg[8 + z], (unsigned long long)ph[z]);
-#endif
-#undef PH
+    PH_END(8, 6);
     if (t0 + nt < P.n) {   // a following table group continues from these cursors
         block_sync();
         for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) O1[(uint64_t)b * nch1 + blockIdx.x] = lcur[b];
@@ -525,12 +528,14 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             if (threadIdx.x < tile_nw(c0, e)) s_tw[threadIdx.x] = src.words[tile_w0(c0) + threadIdx.x];
         }
     }
+    PH_BEGIN(8);
     const uint32_t ntiles = uniform_u32((uint32_t)((c1 - c0 + TILE_KMERS - 1) / TILE_KMERS));
     for (uint32_t ti = 0; ti < ntiles; ti++) {
         const uint64_t j0 = c0 + (uint64_t)ti * TILE_KMERS;
         const uint64_t j1 = min(c1, j0 + TILE_KMERS);
         const bool last = ti + 1 == ntiles;
         block_sync();
+        PH(7);
         TileReads tr = load_tile_reads(src, j0, j1, s_koff, s_meta);
         const uint64_t *tw_cur = s_tw + (ti & 1) * L1F_TW;
         const uint64_t tw_w0 = TW ? tile_w0(j0) : 0;
@@ -581,7 +586,9 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
                 }
             }
         }
+        PH(0);
         block_sync();
+        PH(1);
         // stage region of bucket d: an even number of slots, a leading hole
         // when a record of the bucket is pending (its pair partner), the run,
         // a trailing pad when the run ends unpaired
@@ -592,6 +599,7 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
         block_sync();
         block_scan_hist(lstart, lstart, F1, s_wtot);   // in place: region starts (even)
         block_sync();
+        PH(2);
 #pragma unroll
         for (int q = 0; q < RPT; q++) {
             if (off[q] != ~0u) {
@@ -601,6 +609,14 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
                 sbj[pos] = (b << 16) | ((br[q] >> 23) * L1_THREADS + threadIdx.x);
             }
         }
+        // The next tile's packed words go to their LDS buffer here, not after
+        // the write-out: waiting for that load (vmcnt, which on gfx9 counts
+        // loads and stores together, in order) after this tile's stores would
+        // drain every store of the tile before the closing barrier.  Buffer
+        // (ti + 1) & 1 was last read in tile ti - 1, before this tile's first
+        // barrier; tile ti + 1 reads it after this tile's last one.
+        if (TW && !last && threadIdx.x < L1F_TW) s_tw[((ti + 1) & 1) * L1F_TW + threadIdx.x] = tw_next;
+        PH(3);
         if (!TW && pre) {
             const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
 #pragma unroll
@@ -641,7 +657,9 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             dl[2 * d + 1] = nb + L0 - split - q0;
             qq[d] = make_uint2(q0 + (split - L0), dead ? 0 : q0 + (fe > L0 ? fe - L0 : 0));
         }
+        PH(4);
         block_sync();
+        PH(5);
         // write-out by slot pairs: a pair of records is one 16-B store (its
         // output position is even, inside one block); a (hole, record) or
         // (record, pad) pair writes its record alone, or parks it in the
@@ -670,7 +688,7 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
                 }
             }
         }
-        if (TW && !last && threadIdx.x < L1F_TW) s_tw[((ti + 1) & 1) * L1F_TW + threadIdx.x] = tw_next;
+        PH(6);
         block_sync();
         for (uint32_t d = threadIdx.x; d < F1; d += blockDim.x) {
             const uint32_t h = hist[d];
@@ -683,6 +701,7 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             hist[d] = 0;
         }
     }
+    PH_END(24, 8);
     block_sync();
     for (uint32_t y = threadIdx.x; y < F1 * BLK; y += blockDim.x) {
         const uint32_t d = y >> blk_sh, sl = y & (BLK - 1);
@@ -1240,8 +1259,12 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
     uint32_t *hist = cnt + F2;                      // [F2] this tile's records
     uint32_t *s_nfl = hist + F2;                    // [1] entries of flist (F2 <= THREADS)
     uint16_t *flist = (uint16_t *)(s_nfl + 4);      // [F2] regions whose pending tail completes this tile
+    // A level-1 bucket that overflowed (ctr bit 8) left bkt_cur past its
+    // capacity with unwritten slots below it: nothing of this pass's level 1
+    // may be read; the host redoes the pass on the exact path.
+    if (__builtin_amdgcn_readfirstlane((uint32_t)ctr[CTR_ERR]) & 8u) return;
     const uint32_t b = blockIdx.x / parts, p = blockIdx.x % parts;
-    const uint64_t b0 = bstart[b], b1 = bend[b];
+    const uint64_t b0 = bstart[b], b1 = min(bend[b], bstart[b + 1]);
     const uint64_t len = (b1 - b0 + parts - 1) / parts;
     const uint64_t r0 = min(b1, b0 + (uint64_t)p * len), r1 = min(b1, r0 + len);
     const uint64_t gb = (uint64_t)b << s2;
@@ -1264,11 +1287,13 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
         const uint64_t idx = r0 + (uint64_t)q * THREADS + threadIdx.x;
         v[q] = idx < min(r1, r0 + TILE) ? rec_in[idx] : ~0ull;
     }
+    PH_BEGIN(8);
     const uint32_t ntiles = uniform_u32((uint32_t)((r1 - r0 + TILE - 1) / TILE));
     for (uint32_t ti = 0; ti < ntiles; ti++) {
         const uint64_t t0 = r0 + (uint64_t)ti * TILE;
         const bool last = ti + 1 == ntiles;
         block_sync();
+        PH(7);
         uint32_t rank[RPT];
         uint64_t x[RPT];
 #pragma unroll
@@ -1276,6 +1301,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
             x[q] = v[q];
             if (x[q] != ~0ull) rank[q] = atomicAdd(&hist[(uint32_t)x[q] >> s0], 1u);
         }
+        PH(0);
         {
             const uint64_t n0 = t0 + TILE, n1 = min(r1, n0 + TILE);
 #pragma unroll
@@ -1285,6 +1311,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
             }
         }
         block_sync();
+        PH(1);
         // blocks for this tile (one reservation per region that needs any) and
         // the list of regions whose pending tail segment completes in this
         // tile (every pending one on the last tile); F2 <= THREADS: thread d
@@ -1320,7 +1347,9 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
                 if (fl) flist[base + (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63)) - 1))] = (uint16_t)d;
             }
         }
+        PH(2);
         block_sync();
+        PH(3);
         // flush the listed tails: 16 consecutive lanes per 128-B segment (its
         // slots [a, c0) are this workgroup's, inside its current block)
         {
@@ -1331,7 +1360,9 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
                 if (a + sl < c0) rec_out[bcur[d] + ((a + sl) & (BLK - 1))] = tail[d * SEG + sl];
             }
         }
+        PH(4);
         block_sync();   // the flushed tail slots are refilled below
+        PH(5);
 #pragma unroll
         for (int q = 0; q < RPT; q++) {
             if (x[q] == ~0ull) continue;
@@ -1346,6 +1377,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
                 tail[d * SEG + (L & (SEG - 1))] = val;
             }
         }
+        PH(6);
         block_sync();
         if (threadIdx.x == 0) *s_nfl = 0;
         for (uint32_t d = threadIdx.x; d < F2; d += THREADS) {
@@ -1359,6 +1391,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
             hist[d] = 0;
         }
     }
+    PH_END(32, 8);
     // the rest of every partially filled block: sentinels
     block_sync();
     for (uint32_t y = threadIdx.x; y < F2 * BLK; y += THREADS) {

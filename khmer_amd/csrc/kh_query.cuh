@@ -190,6 +190,22 @@ __global__ void k_median(const uint64_t *koff, uint64_t nreads, uint16_t *counts
     }
 }
 
+// Hashtable::median_at_least (src/oxli/hashtable.cc:333-364), one thread per
+// read over its k-mer counts: the reference's two loops return true exactly
+// when at least min_req = unsigned(0.5 + float(n) / 2) of the n k-mers have a
+// count >= cutoff (the early exits only stop the scan), so the count decides.
+__global__ void k_at_least(const uint64_t *koff, uint64_t nreads, const uint16_t *counts, uint32_t cutoff,
+                           uint8_t *out) {
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < nreads;
+         r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t a = koff[r], n = koff[r + 1] - a;
+        const uint64_t min_req = (uint64_t)(0.5 + (double)((float)n / 2.0f));
+        uint64_t num = 0;
+        for (uint64_t t = 0; t < n; t++) num += (uint32_t)counts[a + t] >= cutoff ? 1 : 0;
+        out[r] = num >= min_req ? 1 : 0;
+    }
+}
+
 // Hashtable::get_median_count over fixed-length device reads, one wave per read
 // (kpr = k-mers per read <= 256, four per lane): the k-mer counts stay in
 // registers.  average: the partial sums are integers below 2^24 (kpr <= 256,

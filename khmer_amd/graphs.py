@@ -38,6 +38,7 @@ class Hashtable(object):
     def __init__(self, k, starting_size, n_tables, primes=None):
         self._g = None
         self._mirrors = None
+        self._views = []
         if primes:
             sizes = [int(p) for p in primes]
         else:
@@ -53,6 +54,7 @@ class Hashtable(object):
         self = cls.__new__(cls)
         self._g = h
         self._mirrors = None
+        self._views = []
         k = ctypes.c_int()
         check(lib.kh_graph_info(h, None, None, ctypes.byref(k), None))
         self._k = k.value
@@ -90,15 +92,23 @@ class Hashtable(object):
     # Host mirrors behind get_raw_tables(): up to this many bytes they are
     # re-copied after every mutating call, so views handed out earlier track
     # the device tables like the reference's aliasing views
-    # (graphs.pyx:333-347); larger tables are re-copied only when
-    # get_raw_tables() is called again (a GB-sized copy per add() would cost
-    # seconds).
+    # (graphs.pyx:333-347).  Larger tables are not re-copied per call (a
+    # GB-sized copy per add() would cost seconds): the views handed out are
+    # released instead, so reading one after a mutating call raises
+    # ValueError rather than returning stale bytes; get_raw_tables() again
+    # gives fresh ones.
     _MIRROR_EAGER_BYTES = 256 << 20
 
     def _refresh_mirrors(self, force=False):
         if not self._mirrors:
             return
         if not force and sum(len(b) for b in self._mirrors) > self._MIRROR_EAGER_BYTES:
+            for v in self._views:
+                try:
+                    v.release()
+                except BufferError:   # re-exported (e.g. numpy.frombuffer): leave it
+                    pass
+            self._views = []
             return
         for i, buf in enumerate(self._mirrors):
             ptr = (ctypes.c_char * len(buf)).from_buffer(buf)
@@ -206,16 +216,24 @@ class Hashtable(object):
         return out.value
 
     def get_kmer_hashes(self, sequence):
-        """Hashes of all k-mers in sequence, in order."""
+        """Hashes of all k-mers in sequence, in order (hashed on the device,
+        Hashtable::get_kmer_hashes, src/oxli/hashtable.cc:378-388)."""
         data = self._valid_sequence(sequence)
         out = (ctypes.c_uint64 * max(len(data), 1))()
         n = ctypes.c_uint64()
-        check(lib.kh_kmer_hashes(self._hash_kind, self._k, data, len(data), out, ctypes.byref(n)))
+        offs = (ctypes.c_uint64 * 2)(0, len(data))
+        check(lib.kh_graph_kmer_hashes(self._g, data, offs, 1, out, ctypes.byref(n)))
         return list(out[:n.value])
 
     def get_kmer_counts(self, sequence):
-        """Retrieve an ordered list of the counts of all k-mers in sequence."""
-        return self._get_counts(self.get_kmer_hashes(sequence))
+        """Retrieve an ordered list of the counts of all k-mers in sequence
+        (hashed and counted on the device, src/oxli/hashtable.cc:403-413)."""
+        data = self._valid_sequence(sequence)
+        out = (ctypes.c_uint16 * max(len(data), 1))()
+        n = ctypes.c_uint64()
+        offs = (ctypes.c_uint64 * 2)(0, len(data))
+        check(lib.kh_graph_kmer_counts(self._g, data, offs, 1, out, ctypes.byref(n)))
+        return list(out[:n.value])
 
     def get_min_count(self, sequence):
         counts = self.get_kmer_counts(sequence)
@@ -252,22 +270,29 @@ class Hashtable(object):
         return [None if st[i] else (med[i], avg[i], sd[i]) for i in range(n)]
 
     def median_at_least(self, sequence, median):
-        """Hashtable::median_at_least (src/oxli/hashtable.cc:333-364)."""
-        data = self._valid_sequence(sequence)
-        counts = self.get_kmer_counts(sequence)
-        min_req = int(0.5 + float(len(data) - self._k + 1) / 2)
-        num = 0
-        for c in counts[:min_req]:
-            if c >= median:
-                num += 1
-        if num >= min_req:
-            return True
-        for c in counts[min_req:]:
-            if c >= median:
-                num += 1
-                if num >= min_req:
-                    return True
-        return False
+        """Check if median k-mer count is at least the given value
+        (Hashtable::median_at_least, src/oxli/hashtable.cc:333-364, on the
+        device)."""
+        self._valid_sequence(sequence)
+        return self.median_at_least_batch([sequence], median)[0]
+
+    def median_at_least_batch(self, sequences, median):
+        """median_at_least over many reads in one device pass (the
+        normalize-by-median filter over a batch).  `median` is converted as
+        the reference's `unsigned int cutoff`.  Reads shorter than k give
+        None (median_at_least raises ValueError for them)."""
+        datas = [s.encode("latin-1") if isinstance(s, str) else bytes(s) for s in sequences]
+        n = len(datas)
+        if not n:
+            return []
+        offs = [0]
+        for d in datas:
+            offs.append(offs[-1] + len(d))
+        out = (ctypes.c_uint8 * n)()
+        st = (ctypes.c_uint8 * n)()
+        check(lib.kh_median_at_least(self._g, b"".join(datas), _u64_array(offs), n, int(median) & 0xFFFFFFFF,
+                                     out, st))
+        return [None if st[i] else bool(out[i]) for i in range(n)]
 
     # ---- files of reads (graphs.pyx:216-296) ----
     def _get_parser(self, parser_or_filename):
@@ -377,13 +402,19 @@ class Hashtable(object):
         return sizes
 
     def get_raw_tables(self):
-        """Read-only memoryviews of the tables.  The views are host mirrors
-        that every later mutating call on this object refreshes, so they track
-        the device tables like the reference's aliasing views."""
+        """Read-only memoryviews of the tables.  The views are host mirrors.
+        Up to 256 MiB of tables, every later mutating call on this object
+        refreshes them, so they track the device tables like the reference's
+        aliasing views (graphs.pyx:333-347).  Above that, a mutating call
+        releases them (reading one raises ValueError); call get_raw_tables()
+        again for current bytes."""
         if self._mirrors is None:
             self._mirrors = [bytearray(n) for n in self._raw_sizes()]
         self._refresh_mirrors(force=True)
-        return [memoryview(b).toreadonly() for b in self._mirrors]
+        views = [memoryview(b).toreadonly() for b in self._mirrors]
+        if sum(len(b) for b in self._mirrors) > self._MIRROR_EAGER_BYTES:
+            self._views.extend(views)
+        return views
 
 
 class Hashgraph(Hashtable):

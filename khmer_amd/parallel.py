@@ -60,6 +60,18 @@ def reinterleave(kind, p, parts):
     return bytes(out)
 
 
+def _slice_bytes(kind, part, size, last):
+    """The bytes rank slice `part` (of `size` bins) contributes to the
+    reference layout (reinterleave, one slice at a time)."""
+    if kind == _lib.STORAGE_BIT:
+        n = size // 8 + (1 if last else 0)
+    elif kind == _lib.STORAGE_NIBBLE:
+        n = size // 2 + (1 if last else 0)
+    else:
+        n = size
+    return bytes(part[:n])
+
+
 def window_owner_range(fj, world, r):
     """k-mer windows [lo, hi) whose winners rank r unions (kh_engine.hip group_wlo)."""
     return fj * r // world, fj * (r + 1) // world
@@ -104,12 +116,25 @@ class _KhTransport(ctypes.Structure):   # include/khmer_hip.h kh_transport
 
 class HostTransport(object):
     """kh_transport over a rendezvous (khmer_amd.rendezvous.Rendezvous or any
-    object with allgather / broadcast / alltoallv of byte strings)."""
+    object with allgather / broadcast / alltoallv of byte strings).  A failed
+    collective is reported to the library (a failed call on this rank) and
+    aborts the rendezvous (if it has abort()), so the peer ranks fail too
+    instead of waiting for this one."""
 
     def __init__(self, rdv):
         self.rdv = rdv
         self.error = None
         world = rdv.world
+
+        def failed(e):
+            self.error = e
+            abort = getattr(rdv, "abort", None)
+            if abort is not None:
+                try:
+                    abort()
+                except Exception:
+                    pass
+            return 1
 
         def allgather(ctx, send, recv, nbytes):
             try:
@@ -117,8 +142,7 @@ class HostTransport(object):
                 ctypes.memmove(recv, b"".join(parts), nbytes * world)
                 return 0
             except Exception as e:   # reported to the library as a failed collective
-                self.error = e
-                return 1
+                return failed(e)
 
         def broadcast(ctx, buf, nbytes, root):
             try:
@@ -127,8 +151,7 @@ class HostTransport(object):
                     ctypes.memmove(buf, data, nbytes)
                 return 0
             except Exception as e:
-                self.error = e
-                return 1
+                return failed(e)
 
         def alltoallv(ctx, send, send_bytes, recv, recv_bytes):
             try:
@@ -148,8 +171,7 @@ class HostTransport(object):
                     at += n
                 return 0
             except Exception as e:
-                self.error = e
-                return 1
+                return failed(e)
 
         self._fns = (_AG(allgather), _BC(broadcast), _A2A(alltoallv))
         self.struct = _KhTransport(None, *self._fns)
@@ -274,10 +296,19 @@ class ShardedCountgraphBench(object):
     def setup(self):
         from . import synth
         from .rendezvous import Rendezvous
+        import os
         a = self.args
         self.rdv = Rendezvous(self.rank, self.world)
-        uid = self.rdv.broadcast(ShardedGraph.unique_id() if self.rank == 0 else b"", 0)
-        self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device, uid=uid)
+        # RCCL (one GPU per rank); "host": the collectives through host memory
+        # and the rendezvous -- the dry run of several ranks on one device
+        # (KH_BENCH_DEVICE), which RCCL refuses ("Duplicate GPU detected")
+        self.transport = os.environ.get("KH_BENCH_TRANSPORT", "host" if "KH_BENCH_DEVICE" in os.environ else "rccl")
+        if self.transport == "host":
+            self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device,
+                                  transport=HostTransport(self.rdv))
+        else:
+            uid = self.rdv.broadcast(ShardedGraph.unique_id() if self.rank == 0 else b"", 0)
+            self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device, uid=uid)
         nranks, dev = self.g.comm_info()
         self.comm = [tuple(int(x) for x in p.split(b",")) for p in
                      self.rdv.allgather(b"%d,%d,%d" % (self.rank, nranks, dev))]
@@ -324,6 +355,23 @@ class ShardedCountgraphBench(object):
         for line in buf.value.decode().splitlines():
             name, cnt, ms = line.split("\t")
             out[name] = (int(cnt), float(ms))
+        return out
+
+    def table_sha256(self):
+        """SHA-256 of every reference-layout table, computed on rank 0 from
+        the rank slices streamed to it in rank order (collective; None on the
+        other ranks)."""
+        import hashlib
+        mine = self.g.local_tables()[0]
+        out = []
+        for i, p in enumerate(self.sizes):
+            h = hashlib.sha256() if self.rank == 0 else None
+            for r in range(self.world):
+                blob = self.rdv.send_to_root(mine[i] if self.rank == r else b"", r)
+                if h is not None:
+                    size = shard_lo(p, self.world, r + 1) - shard_lo(p, self.world, r)
+                    h.update(_slice_bytes(self.g.kind, blob, size, r == self.world - 1))
+            out.append(h.hexdigest() if h is not None else None)
         return out
 
     def check(self):

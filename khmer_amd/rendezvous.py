@@ -9,6 +9,11 @@ the same order.  Messages are length-prefixed byte strings (no pickling).
 
 Address: MASTER_ADDR (default 127.0.0.1); port: KH_RDV_PORT, else MASTER_PORT
 + 1 (torchrun's own store listens on MASTER_PORT).
+
+Failure: every socket operation has a finite timeout (`op_timeout`,
+KH_RDV_OP_TIMEOUT seconds, default 900), and `abort()` closes this rank's
+connections, so a rank whose collective failed makes its peers fail with
+ConnectionError instead of waiting forever.
 """
 import os
 import socket
@@ -42,8 +47,10 @@ def _recv(sock):
 class Rendezvous(object):
     """Star-shaped TCP group of `world` ranks served by rank 0."""
 
-    def __init__(self, rank, world, addr=None, port=None, timeout=600.0):
+    def __init__(self, rank, world, addr=None, port=None, timeout=600.0, op_timeout=None):
         self.rank, self.world = int(rank), int(world)
+        if op_timeout is None:
+            op_timeout = float(os.environ.get("KH_RDV_OP_TIMEOUT", "900"))
         addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
         if port is None:
             port = int(os.environ.get("KH_RDV_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
@@ -61,7 +68,7 @@ class Rendezvous(object):
                 while len(self.peers) < self.world - 1:
                     c, _ = srv.accept()
                     c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                    c.settimeout(None)
+                    c.settimeout(op_timeout)
                     (r,) = struct.unpack("<i", _recv_exact(c, 4))
                     self.peers[r] = c
             finally:
@@ -77,7 +84,7 @@ class Rendezvous(object):
                         raise
                     time.sleep(0.1)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            s.settimeout(None)
+            s.settimeout(op_timeout)
             s.sendall(struct.pack("<i", self.rank))
             self.sock = s
 
@@ -144,11 +151,26 @@ class Rendezvous(object):
             at += n
         return out
 
+    def send_to_root(self, data, src):
+        """Rank `src`'s bytes on rank 0 (b"" elsewhere)."""
+        if self.world == 1 or src == 0:
+            return bytes(data) if self.rank == 0 else b""
+        if self.rank == 0:
+            return _recv(self.peers[src])
+        if self.rank == src:
+            _send(self.sock, bytes(data))
+        return b""
+
     def barrier(self):
         self.allgather(b"")
 
     def max(self, x):
         return max(struct.unpack("<d", p)[0] for p in self.allgather(struct.pack("<d", float(x))))
+
+    def abort(self):
+        """Drop this rank's connections after a failed collective: peers
+        blocked on it get ConnectionError (or their timeout) and fail too."""
+        self.close()
 
     def close(self):
         for c in self.peers.values():

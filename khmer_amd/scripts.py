@@ -5,17 +5,43 @@
 scripts/load-graph.py (reference scripts/load-graph.py + oxli/build_graph.py:
 40-123).  Options, stderr messages, the saved table, the `.info` file, the
 `.info.json` / `.info.tsv` summaries and the `.tagset` file match the
-reference's.  Each input file is consumed by one device call
-(Countgraph.consume_seqfile -> kh_consume_parser); `-T` is accepted and has no
-effect on the result, as with the reference (its threads only share one
-parser).  The tests call these functions in-process; the files under
-scripts/ are two-line wrappers.
+reference's.  Each input file is consumed as the reference does it: `-T`
+Python threads all call consume_seqfile[_and_tag] on one shared ReadParser
+(scripts/load-into-counting.py:143-158, oxli/functions.py:56-66).  The first
+call drains the parser into the device pipeline; the others find it drained
+and return their (empty) share, so the tables and counters do not depend on
+-T.  One deliberate difference: an exception in a consuming thread is
+re-raised in the main thread after the join (the reference's thread prints
+it and the script carries on).  The tests call these functions in-process;
+the files under scripts/ are two-line wrappers.
 """
 import json
 import os
 import sys
+import threading
 
 from . import khmer_args as KA
+
+
+def consume_threads(eat, parser, num_threads):
+    """`num_threads` threads calling eat(parser) on one shared parser; their
+    (reads, k-mers) shares, and the first exception re-raised after the join."""
+    shares, errors = [], []
+
+    def run():
+        try:
+            shares.append(eat(parser))
+        except BaseException as e:   # re-raised in the caller below
+            errors.append(e)
+
+    threads = [threading.Thread(target=run) for _ in range(max(1, int(num_threads)))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    return shares
 
 
 # ---------------------------------------------------------------------------
@@ -93,7 +119,7 @@ def load_into_counting(argv=None):
     for index, filename in enumerate(filenames):
         parser = khmer_amd.ReadParser(filename)
         KA.log_info("consuming input {input}", input=filename)
-        countgraph.consume_seqfile(parser)
+        consume_threads(countgraph.consume_seqfile, parser, args.threads)
         if index > 0 and index % 10 == 0:     # periodic checkpoint, as the reference
             KA.check_space_for_graph(base, KA.calculate_graphsize(args, "countgraph"), args.force)
             KA.log_info("mid-save {base}", base=base)
@@ -155,7 +181,7 @@ def build_graph(filenames, graph, num_threads=1, tags=False):
     eat = graph.consume_seqfile_and_tag if tags else graph.consume_seqfile
     for name in filenames:
         parser = khmer_amd.ReadParser(name)
-        eat(parser)
+        consume_threads(eat, parser, num_threads)
         parser.close()
 
 

@@ -997,3 +997,19 @@ uint64_t or_consume_synth(or_table *t, uint64_t seed, uint64_t genome, uint64_t 
     free(buf);
     return total;
 }
+
+/* get_median_count (or_median, src/oxli/hashtable.cc:299-328) of reads
+ * r0..r0+nreads-1 of a synthetic stream, one output triple per read (the
+ * golden fixtures' query digests) */
+int or_median_synth(const or_table *t, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L,
+                    uint16_t *med, float *avg, float *sd) {
+    char *buf = malloc((size_t)L + 1);
+    int rc = 0;
+    for (uint64_t r = 0; r < nreads && rc == 0; r++) {
+        if (genome) or_synth_genomic_read(seed, genome, r0 + r, L, buf);
+        else or_synth_read(seed, r0 + r, L, buf);
+        rc = or_median(t, buf, (size_t)L, &med[r], &avg[r], &sd[r]);
+    }
+    free(buf);
+    return rc;
+}

@@ -76,6 +76,7 @@ def lib():
             "or_synth_read": (None, [u64, u64, i32, ctypes.c_char_p]),
             "or_synth_genomic_read": (None, [u64, u64, u64, i32, ctypes.c_char_p]),
             "or_consume_synth": (u64, [P, u64, u64, u64, u64, i32]),
+            "or_median_synth": (i32, [P, u64, u64, u64, u64, i32, P, P, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -211,6 +212,18 @@ class Table:
         """Consume reads r0.. of the benchmark's synthetic stream (khmer_amd/synth.py),
         in stream order; genome > 0 selects the genomic stream."""
         return lib().or_consume_synth(self._h, seed, genome, r0, nreads, length)
+
+    def median_synth(self, seed, r0, nreads, length, genome=0):
+        """get_median_count of reads r0.. of the synthetic stream: numpy
+        (median u16, average f32, stddev f32) arrays."""
+        import numpy as np
+        med = np.zeros(nreads, np.uint16)
+        avg = np.zeros(nreads, np.float32)
+        sd = np.zeros(nreads, np.float32)
+        if lib().or_median_synth(self._h, seed, genome, r0, nreads, length, med.ctypes.data, avg.ctypes.data,
+                                 sd.ctypes.data) != 0:
+            raise ValueError(err())
+        return med, avg, sd
 
     def table_view(self, i):
         """Zero-copy read-only view of table i (for digests of GB tables)."""

@@ -48,6 +48,23 @@ def bigcount_digest(d):
     return len(keys), hashlib.sha256(blob).hexdigest()
 
 
+def median_digest(med, avg, sd):
+    """SHA-256 of get_median_count's outputs over a read range: the u16
+    medians, then the f32 averages, then the f32 stddevs (little-endian
+    arrays, bit patterns exactly)."""
+    import numpy as np
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(med, dtype="<u2").tobytes())
+    h.update(np.ascontiguousarray(avg, dtype="<f4").tobytes())
+    h.update(np.ascontiguousarray(sd, dtype="<f4").tobytes())
+    return h.hexdigest()
+
+
+# get_median_count digests over the first MEDIAN_READS reads of the stream,
+# for the configurations whose query path the bench measures (C5 / C5M)
+MEDIAN_READS = {"c5_shape": 1_000_000, "c5m_shape": 1_000_000}
+
+
 def fixture_path(name):
     return os.path.join(FULL, name + ".json")
 

@@ -40,6 +40,14 @@ def make(name):
         "n_bigcounts": nbc, "bigcount_sha256": bcd,
         "generator": "tests/golden/make_full_fixtures.py (oracle, 1 thread, %.0f s)" % secs,
     }
+    nmed = FD.MEDIAN_READS.get(name)
+    if nmed:
+        t0 = time.time()
+        med, avg, sd = t.median_synth(synth.SEED, 0, nmed, c["L"], genome=c["genome"])
+        out["median_reads"] = nmed
+        out["median_sha256"] = FD.median_digest(med, avg, sd)
+        out["median_max"] = int(med.max())
+        out["generator"] += ", median digest %.0f s" % (time.time() - t0)
     os.makedirs(FD.FULL, exist_ok=True)
     with open(FD.fixture_path(name), "w") as fh:
         json.dump(out, fh, indent=1)

@@ -1,0 +1,64 @@
+"""bench.py's host-side logic on CPU: the golden-fixture match that makes a
+bench line carry its own parity check (VERDICT r2 "Next round" #1c), and the
+algorithmic-bytes figures of SURVEY.md §8(d)."""
+import importlib.util
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _args(bench, argv):
+    old = sys.argv
+    sys.argv = ["bench.py"] + argv
+    try:
+        return bench.parse()
+    finally:
+        sys.argv = old
+
+
+def test_default_workload_is_c2_full(bench):
+    a = _args(bench, [])
+    fx = bench.matching_fixture(a, a.reads)
+    assert fx is not None and fx["config"] == "c2_full"
+    # strong scaling over 8 ranks is the same stream
+    a8 = _args(bench, ["--gpus", "8", "--strong"])
+    assert bench.matching_fixture(a8, 8 * ((a8.reads + 7) // 8))["config"] == "c2_full"
+    # weak scaling at 8 ranks: 400M reads, no fixture
+    assert bench.matching_fixture(a8, 8 * a8.reads) is None
+
+
+@pytest.mark.parametrize("argv,name", [(["--config", "C3", "--reads", "4000000"], "c3_shape"),
+                                       (["--config", "C4", "--reads", "4000000"], "c4_shape"),
+                                       (["--config", "C5", "--reads", "4000000"], "c5_shape"),
+                                       (["--genome", "2e6", "--reads", "10000000"], "genomic_c2"),
+                                       (["--reads", "49999999"], None),
+                                       (["--no-bigcount"], None)])
+def test_fixture_match(bench, argv, name):
+    a = _args(bench, argv)
+    fx = bench.matching_fixture(a, a.reads)
+    assert (fx["config"] if fx else None) == name
+
+
+def test_compare_fixture(bench):
+    a = _args(bench, [])
+    fx = bench.matching_fixture(a, a.reads)
+    ok = bench.compare_fixture(fx, fx["n_unique_kmers"], fx["n_occupied"], fx["table_sha256"])
+    assert ok == {"fixture": "c2_full", "counters_match": True, "tables_match": True}
+    bad = bench.compare_fixture(fx, fx["n_unique_kmers"] + 1, fx["n_occupied"], None)
+    assert bad == {"fixture": "c2_full", "counters_match": False}
+
+
+def test_algorithmic_bytes(bench):
+    assert abs(bench.algorithmic_bytes_per_kmer(150, 21, 4) - 8.288461538) < 1e-6
+    assert abs(bench.query_bytes_per_kmer(150, 51, 4) - 4.475) < 1e-9

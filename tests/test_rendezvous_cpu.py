@@ -77,3 +77,49 @@ def test_single_rank_is_local():
     r = Rendezvous(0, 1)
     assert r.allgather(b"x") == [b"x"] and r.broadcast(b"y") == b"y" and r.alltoallv([b"z"]) == [b"z"]
     assert r.max(2.5) == 2.5
+
+
+def _failing_worker(rank, world, port, q):
+    """Rank 1's alltoallv callback fails (wrong receive sizes): it returns 1
+    and aborts the rendezvous, and the other ranks' next collective fails
+    (returns 1) instead of waiting forever (peers blocked in recv)."""
+    try:
+        import time
+        from khmer_amd.rendezvous import Rendezvous
+        from khmer_amd.parallel import HostTransport
+        rdv = Rendezvous(rank, world, "127.0.0.1", port, timeout=60, op_timeout=30)
+        st = HostTransport(rdv).struct
+        sb = (ctypes.c_uint64 * world)(*[4] * world)
+        sa = (ctypes.c_uint32 * world)(*range(world))
+        rb = (ctypes.c_uint64 * world)(*([8 if rank == 1 else 4] * world))
+        ra = (ctypes.c_uint32 * (2 * world))()
+        first = st.alltoallv(None, ctypes.addressof(sa), sb, ctypes.addressof(ra), rb)
+        t0 = time.time()
+        send = (ctypes.c_uint64 * 1)(rank)
+        recv = (ctypes.c_uint64 * world)()
+        second = st.allgather(None, ctypes.addressof(send), ctypes.addressof(recv), 8) if rank != 1 else 1
+        q.put((rank, first, second, time.time() - t0))
+    except Exception as e:   # reported to the parent
+        q.put((rank, -1, -1, repr(e)))
+
+
+def test_failed_collective_fails_the_peers():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res[1][1] == 1                                   # rank 1's own failure
+    assert all(r[2] == 1 for r in res), res                 # everyone's next collective fails ...
+    assert all(r[3] < 25 for r in res if r[0] != 1), res    # ... promptly (not at the op timeout)
+
+
+def test_send_to_root_single():
+    from khmer_amd.rendezvous import Rendezvous
+    r = Rendezvous(0, 1)
+    assert r.send_to_root(b"abc", 0) == b"abc"

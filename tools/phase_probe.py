@@ -1,5 +1,7 @@
-"""Timing probe (development only): runs the C2 bench workload for one step
-and prints the per-phase cycle counters a debug build accumulates."""
+"""Timing probe (development only): runs the C2 bench workload and prints the
+per-phase cycle counters a -DKH_PHASES build accumulates (tools/build_variant.sh
+phases "-DKH_PHASES"; run with KHMER_AMD_LIB=ab/libphases.so).  Each kernel's
+phases are s_memtime stamps summed over workgroups (kh_partition.cuh PH_*)."""
 import ctypes
 import os
 import sys
@@ -9,11 +11,20 @@ import khmer_amd  # noqa: E402
 from khmer_amd import synth  # noqa: E402
 from khmer_amd._lib import lib, check  # noqa: E402
 
+PHASES = {
+    "scatter_l1 (exact)": (8, ["tile top", "hash+rank", "scan", "stage", "tails", "write"]),
+    "apply": (16, ["records", "pass-1 wait", "winner scan", "write-back", "pass 1", "init"]),
+    "scatter_l1f": (24, ["hash+rank", "barrier 1", "starts+scan", "stage", "reserve", "barrier 2", "write-out",
+                         "advance+top barrier"]),
+    "scatter_l2f": (32, ["wait+rank", "prefetch+barrier", "reserve+flist", "barrier", "flush", "barrier",
+                         "stores", "advance+top barrier"]),
+}
+
 reads = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 L, k = 150, 21
 g = khmer_amd.Countgraph(k, 1e9, 4)
 g.set_use_bigcount(True)
-check(lib.kh_graph_set_batch_kmers(g._g, 1 << 30))
+check(lib.kh_graph_set_batch_kmers(g._g, 2560 << 20))
 words, koff = ctypes.c_void_p(), ctypes.c_void_p()
 check(lib.kh_device_malloc(0, reads * L // 32 * 8 + 64, ctypes.byref(words)))
 check(lib.kh_device_malloc(0, (reads + 1) * 8, ctypes.byref(koff)))
@@ -25,4 +36,11 @@ for it in range(2):
     check(lib.kh_consume_packed_fixed_device(g._g, words, reads, L))
     check(lib.kh_device_synchronize(0))
     lib.kh_debug_read(dbg)
-    print("iter", it, "phases:", " ".join("%d:%.3e" % (i, dbg[i]) for i in range(64) if dbg[i]), flush=True)
+    print("iter", it, flush=True)
+    for name, (base, labels) in PHASES.items():
+        vals = [dbg[base + i] for i in range(len(labels))]
+        tot = sum(vals)
+        if not tot:
+            continue
+        print("  %-20s %s" % (name, "  ".join("%s %.1f%%" % (lab, 100.0 * v / tot) for lab, v in zip(labels, vals))),
+              flush=True)
