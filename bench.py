@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("-k", type=int, default=None, help="override the preset's k")
     ap.add_argument("--tables", type=int, default=4)
     ap.add_argument("-x", type=float, default=None, help="override the preset's table size")
-    ap.add_argument("--batch-kmers", type=int, default=2560 << 20,
+    ap.add_argument("--batch-kmers", type=int, default=3200 << 20,
                     help="largest device pass (the library cap, MAX_PASS_KMERS); fewer, larger passes "
                          "amortise the per-bin work of every pass")
     ap.add_argument("--no-bigcount", action="store_true")
@@ -466,9 +466,12 @@ class SingleGpuBench(object):
             check(lib.kh_synth_packed_device(self.device, synth.SEED, 0, a.reads, a.read_len, ks, self.words,
                                              self.koff))
         self.reads = self.words
-        if a.murmur:   # Counttable family: the same bases as ASCII
+        if a.murmur:   # Counttable family: the same bases as ASCII (the packed words are then freed)
             self.reads = self._alloc(a.reads * a.read_len + 64)
             check(lib.kh_unpack_ascii_device(self.device, self.words, a.reads * a.read_len, self.reads))
+            check(lib.kh_device_free(self.device, self.words))
+            self.bufs.remove(self.words)
+            self.words = None
         if a.query:
             self.med = self._alloc(a.reads * 2 + 64)
             self.avg = self._alloc(a.reads * 4 + 64)

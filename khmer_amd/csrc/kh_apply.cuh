@@ -34,7 +34,16 @@ struct ApplyArgs {
     uint4 *xseg;
     uint64_t *ctr;
     uint64_t rprefix[MAXT + 1];   // real-region prefix per table
+    // coarse-window winners (unsharded passes): instead of per-region lists,
+    // every region's winners are counting-sorted in LDS by coarse k-mer
+    // window (j >> cjs, <= 64 windows) and appended as runs to that window's
+    // range of wco: [cw_cur[c] at the start, its capacity end) -- the capacity
+    // is the window's k-mers x tables, a hard bound on its winners
+    int coarse, cjs;
+    uint32_t *wco;
+    unsigned long long *cw_cur;
 };
+constexpr int MAX_CW = 64;
 
 __device__ __forceinline__ void full_add(uint8_t *fullf, uint32_t j) {
     atomicAdd((uint32_t *)(fullf + (j & ~3u)), 1u << (8 * (j & 3u)));
@@ -362,7 +371,77 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
             }
         }
         uint32_t wall;
-        uint64_t pos = ri.e0 + winner_base(s_wt, &wall) + wex;
+        uint32_t pos = winner_base(s_wt, &wall) + wex;
+        uint32_t *wst = cnt;
+        if (A.coarse) {
+            // coarse-window runs: per-window counts (LDS atomics), a wave-0
+            // scan and one returning global atomic per non-empty window, the
+            // winners placed window by window in LDS (the dead count array),
+            // then every run written by consecutive lanes.  full255 (bigcount
+            // bookkeeping, read above) holds the window counters.
+            uint32_t *chist = full255, *cst0 = full255 + MAX_CW;
+            unsigned long long *cgb = (unsigned long long *)(full255 + 2 * MAX_CW);
+            const int cjs = A.cjs;
+            block_sync();   // full255's last readers (the loop above) are done
+            if (t < MAX_CW) chist[t] = 0;
+            block_sync();
+            if (nw) {
+#pragma unroll
+                for (int step = 0; step < BPT / 4; step++) {
+                    const uint32_t g = t + (uint32_t)step * TH;
+                    const uint32_t win = wflag[g];
+                    if (!win) continue;
+                    const uint4 m = ((const uint4 *)minj)[g];
+                    if (win & 1) atomicAdd(&chist[m.x >> cjs], 1u);
+                    if (win & 2) atomicAdd(&chist[m.y >> cjs], 1u);
+                    if (win & 4) atomicAdd(&chist[m.z >> cjs], 1u);
+                    if (win & 8) atomicAdd(&chist[m.w >> cjs], 1u);
+                }
+            }
+            block_sync();
+            if (t < 64) {
+                const uint32_t c = chist[t];
+                uint32_t incl = c;
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = __shfl_up(incl, d, 64);
+                    if (t >= (uint32_t)d) incl += y;
+                }
+                cst0[t] = incl - c;
+                cgb[t] = c ? atomicAdd(&A.cw_cur[t], (unsigned long long)c) : 0ull;
+                chist[t] = 0;   // placement cursors
+            }
+            block_sync();
+            if (nw) {
+#pragma unroll
+                for (int step = 0; step < BPT / 4; step++) {
+                    const uint32_t g = t + (uint32_t)step * TH;
+                    const uint32_t win = wflag[g];
+                    if (!win) continue;
+                    const uint4 m = ((const uint4 *)minj)[g];
+                    const uint32_t mv[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if (win & (1u << k)) {
+                            const uint32_t c = mv[k] >> cjs;
+                            wst[cst0[c] + atomicAdd(&chist[c], 1u)] = mv[k];
+                        }
+                }
+            }
+            if (t == 0) A.wcnt[rr] = wall;
+            block_sync();
+            for (uint32_t x = t; x < wall; x += TH) {
+                const uint32_t v = wst[x], c = v >> cjs;
+                A.wco[cgb[c] + (x - cst0[c])] = v;
+            }
+            block_sync();
+            PH(3);
+            cur = nxt;
+            continue;
+        }
+        // winners: staged in LDS in region order (the count array is dead
+        // after pass 1), then written to the region's segment by consecutive
+        // lanes -- coalesced, where each lane writing its own run directly
+        // scatters every store instruction over ~64 lines
         if (nw) {
 #pragma unroll
             for (int step = 0; step < BPT / 4; step++) {
@@ -370,13 +449,15 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
                 const uint32_t win = wflag[g];
                 if (!win) continue;
                 const uint4 m = ((const uint4 *)minj)[g];
-                if (win & 1) A.win[pos++] = m.x;
-                if (win & 2) A.win[pos++] = m.y;
-                if (win & 4) A.win[pos++] = m.z;
-                if (win & 8) A.win[pos++] = m.w;
+                if (win & 1) wst[pos++] = m.x;
+                if (win & 2) wst[pos++] = m.y;
+                if (win & 4) wst[pos++] = m.z;
+                if (win & 8) wst[pos++] = m.w;
             }
         }
         if (t == 0) A.wcnt[rr] = wall;
+        block_sync();
+        for (uint32_t x = t; x < wall; x += TH) A.win[ri.e0 + x] = wst[x];
         block_sync();
         PH(3);
         cur = nxt;
@@ -618,6 +699,138 @@ __global__ void __launch_bounds__(PT_THREADS) k_mark(const uint32_t *wout, const
         const uint4 x = ((const uint4 *)bits)[t];
         uniq += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
         if (newbits) ((uint4 *)(newbits + (uint64_t)jb * nw))[t] = x;
+    }
+    uniq = wave_sum(uniq);
+    if ((threadIdx.x & 63) == 0 && uniq) atomicAdd((unsigned long long *)&ctr[CTR_UNIQUE], (unsigned long long)uniq);
+}
+
+// ---------------------------------------------------------------------------
+// Coarse-window winners -> fine windows of 2^js k-mers -> LDS bitmaps.  A
+// chunk is a contiguous slice of one coarse window's winners (host-planned
+// from the windows' counts); the count matrix is laid out [coarse][fine][chunk]
+// so one exclusive scan gives every (fine window, chunk) its output offset and
+// every fine window one contiguous range.
+struct WChunk {
+    uint64_t start, end;     // winners [start, end) of wco
+    uint64_t mbase;          // chunk_prefix(coarse) * fpc
+    uint32_t k, nk;          // chunk index inside its coarse window, chunks of that window
+};
+constexpr int WF_THREADS = 1024;
+constexpr int WF_RPT = 8;
+constexpr int WF_TILE = WF_THREADS * WF_RPT;
+constexpr uint32_t WF_CHUNK = 16 * WF_TILE;   // winners per chunk
+
+__global__ void __launch_bounds__(WF_THREADS) k_hist_wf(const uint32_t *wco, const WChunk *chunks, int js,
+                                                        uint32_t fpc, uint32_t *M) {
+    __shared__ uint32_t hist[MAX_CW];
+    const WChunk ch = chunks[blockIdx.x];
+    if (threadIdx.x < MAX_CW) hist[threadIdx.x] = 0;
+    block_sync();
+    // eight loads in flight per thread
+    for (uint64_t i0 = ch.start; i0 < ch.end; i0 += 8 * WF_THREADS) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint64_t i = i0 + (uint64_t)u * WF_THREADS + threadIdx.x;
+            v[u] = i < ch.end ? wco[i] : NO_J;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (v[u] != NO_J) atomicAdd(&hist[(v[u] >> js) & (fpc - 1)], 1u);
+    }
+    block_sync();
+    if (threadIdx.x < fpc) M[ch.mbase + (uint64_t)threadIdx.x * ch.nk + ch.k] = hist[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(WF_THREADS) k_scatter_wf(const uint32_t *wco, const WChunk *chunks, int js,
+                                                           uint32_t fpc, const uint64_t *O, uint32_t *wout) {
+    __shared__ uint32_t stage[WF_TILE];
+    __shared__ uint32_t hist[MAX_CW], lstart[MAX_CW];
+    __shared__ uint64_t cur[MAX_CW];
+    const WChunk ch = chunks[blockIdx.x];
+    if (threadIdx.x < fpc) {
+        cur[threadIdx.x] = O[ch.mbase + (uint64_t)threadIdx.x * ch.nk + ch.k];
+        hist[threadIdx.x] = 0;
+    }
+    const uint32_t ntiles = uniform_u32((uint32_t)((ch.end - ch.start + WF_TILE - 1) / WF_TILE));
+    for (uint32_t ti = 0; ti < ntiles; ti++) {
+        const uint64_t t0 = ch.start + (uint64_t)ti * WF_TILE;
+        block_sync();
+        uint32_t v[WF_RPT], rank[WF_RPT];
+#pragma unroll
+        for (int q = 0; q < WF_RPT; q++) {
+            const uint64_t i = t0 + (uint64_t)q * WF_THREADS + threadIdx.x;
+            v[q] = i < ch.end ? wco[i] : NO_J;
+            if (v[q] != NO_J) rank[q] = atomicAdd(&hist[(v[q] >> js) & (fpc - 1)], 1u);
+        }
+        block_sync();
+        if (threadIdx.x < 64) {
+            const uint32_t c = threadIdx.x < fpc ? hist[threadIdx.x] : 0;
+            uint32_t incl = c;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(incl, d, 64);
+                if (threadIdx.x >= (uint32_t)d) incl += y;
+            }
+            if (threadIdx.x < fpc) lstart[threadIdx.x] = incl - c;
+        }
+        block_sync();
+#pragma unroll
+        for (int q = 0; q < WF_RPT; q++)
+            if (v[q] != NO_J) stage[lstart[(v[q] >> js) & (fpc - 1)] + rank[q]] = v[q];
+        block_sync();
+        const uint32_t n = (uint32_t)min((uint64_t)WF_TILE, ch.end - t0);
+        for (uint32_t x = threadIdx.x; x < n; x += WF_THREADS) {
+            const uint32_t vv = stage[x], f = (vv >> js) & (fpc - 1);
+            wout[cur[f] + (x - lstart[f])] = vv;
+        }
+        block_sync();
+        if (threadIdx.x < fpc) {
+            cur[threadIdx.x] += hist[threadIdx.x];
+            hist[threadIdx.x] = 0;
+        }
+    }
+}
+
+// one workgroup per fine window: its winners' LDS bitmap -> n_unique (and the
+// per-k-mer new flags when asked); range [O[mbase(c) + f*nk_c], next)
+__global__ void __launch_bounds__(PT_THREADS) k_mark_wf(const uint32_t *wout, const uint64_t *O,
+                                                        const uint64_t *cmbase, const uint32_t *cnk, uint32_t fpc,
+                                                        int js, uint64_t *ctr, uint32_t *newbits) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *bits = (uint32_t *)smem;   // [2^js / 32]
+    const uint32_t nw = 1u << (js - 5);
+    const uint32_t fw = blockIdx.x, c = fw / fpc, f = fw % fpc;
+    const uint32_t nk = cnk[c];
+    uint64_t s = 0, e = 0;
+    if (nk) {   // O has one entry past the matrix (the total): (c, f + 1)'s start ends (c, f)
+        s = O[cmbase[c] + (uint64_t)f * nk];
+        e = O[cmbase[c] + (uint64_t)(f + 1) * nk];
+    }
+    for (uint32_t t = threadIdx.x; t < nw / 4; t += blockDim.x) ((uint4 *)bits)[t] = make_uint4(0, 0, 0, 0);
+    block_sync();
+    const uint32_t mask = (1u << js) - 1;
+    // eight loads in flight per thread (one per iteration left the window's
+    // stream latency-bound at ~2 TB/s)
+    for (uint64_t q0 = s; q0 < e; q0 += 8 * (uint64_t)blockDim.x) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint64_t q = q0 + (uint64_t)u * blockDim.x + threadIdx.x;
+            v[u] = q < e ? wout[q] : NO_J;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (v[u] != NO_J) {
+                const uint32_t j = v[u] & mask;
+                atomicOr(&bits[j >> 5], 1u << (j & 31));
+            }
+    }
+    block_sync();
+    uint64_t uniq = 0;
+    for (uint32_t t = threadIdx.x; t < nw / 4; t += blockDim.x) {
+        const uint4 x = ((const uint4 *)bits)[t];
+        uniq += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+        if (newbits) ((uint4 *)(newbits + (uint64_t)fw * nw))[t] = x;
     }
     uniq = wave_sum(uniq);
     if ((threadIdx.x & 63) == 0 && uniq) atomicAdd((unsigned long long *)&ctr[CTR_UNIQUE], (unsigned long long)uniq);

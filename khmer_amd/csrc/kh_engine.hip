@@ -70,7 +70,7 @@ static PassGeo pass_geo(const Params &P, uint64_t nkmers) {
     q.ck1 = 32768u * ((P.F1 + 1023) / 1024);
     q.nch1 = (uint32_t)((nkmers + q.ck1 - 1) / q.ck1);
     q.nch2max = q.recs / L2_CHUNK + P.F1 + 1;
-    q.js = std::min(20, std::max(17, ceil_log2(nkmers) - 11));   // <= 2560 windows of <= 2^20 k-mers
+    q.js = std::min(20, std::max(17, ceil_log2(nkmers) - 11));   // <= 3200 windows of <= 2^20 k-mers
     q.FJ = (uint32_t)((nkmers + (1ull << q.js) - 1) >> q.js);
     q.regions = 0;
     for (int i = 0; i < P.n; i++) q.regions += (P.lsz[i] + (1ull << P.s0) - 1) >> P.s0;
@@ -215,7 +215,7 @@ static bool l2f_wanted(const Graph *g, uint64_t nkmers) {
 static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
     Workspace &w = g->ws;
     const Params &P = g->prm;
-    if (w.reg_base && w.reg_nkmers == nkmers) return w.reg_total;
+    if (w.reg_base && w.reg_nkmers == nkmers && w.reg_sigma == g->cap_sigma) return w.reg_total;
     const uint64_t nreg = (uint64_t)P.F1 << P.s2;
     const uint64_t R = 1ull << P.s0;
     const uint64_t slack = (uint64_t)(l2f_parts(P.F1) + 1) * (1ull << l2f_blk_sh()) + 16;
@@ -229,7 +229,7 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
         if (lo >= P.tbase[i] + P.lsz[i]) continue;   // padding up to the next bucket boundary
         const uint64_t nb = std::min<uint64_t>(R, P.tbase[i] + P.lsz[i] - lo);
         const double mean = (double)nkmers * (double)nb / (double)P.p[i];
-        uint64_t c = (uint64_t)(mean + 8.0 * sqrt(mean)) + slack;
+        uint64_t c = (uint64_t)(mean + g->cap_sigma * sqrt(mean)) + slack;
         acc += (c + 15) & ~15ull;
     }
     base[nreg] = acc;
@@ -240,6 +240,7 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
     ensure((void **)&w.reg_cur, &cap_cur, nreg, 8);
     KH_HIP(hipMemcpy(w.reg_base, base.data(), (nreg + 1) * 8, hipMemcpyHostToDevice));
     w.reg_nkmers = nkmers;
+    w.reg_sigma = g->cap_sigma;
     w.reg_total = acc;
     return acc;
 }
@@ -247,7 +248,7 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
 // ---- fixed-capacity level 1 (k_scatter_l1f) ----
 // up to 1024 buckets (the per-bucket LDS state), hashed sources with <= 8
 // tables per launch; not for shards using the owned-record filter
-static int env_seg(const char *name, int dflt) {   // development: KH_L2_SEG / KH_W_SEG tail sizes
+static int env_seg(const char *name, int dflt) {   // development knobs
     const char *e = getenv(name);
     return e && *e ? atoi(e) : dflt;
 }
@@ -269,9 +270,9 @@ static uint32_t device_cus(const Graph *g) {
 }
 // a persistent grid: two workgroups per CU (the kernel's LDS allows two at up
 // to ~512 buckets), fewer for small passes
-// records per thread and tile: 8 (3 workgroups per CU) or 16 (2 workgroups,
-// twice the tile); KH_L1F_RPT (development)
-static int l1f_rpt() { static const int v = env_seg("KH_L1F_RPT", L1_MAX_RPT) == 16 ? 16 : L1_MAX_RPT; return v; }
+// records per thread and tile: 8 (3 workgroups per CU; 16 records with 2
+// workgroups per CU measured slower, 117 vs 112 ms/step, round 2)
+static int l1f_rpt() { return L1_MAX_RPT; }
 static size_t lds_scatter_l1f(const Params &P, bool window, int tile_kmers) {
     const size_t F1a = (P.F1 + 3) & ~3u;
     const size_t tile = (size_t)L1_THREADS * l1f_rpt();
@@ -284,7 +285,7 @@ static uint32_t l1f_wpc(const Params &P) {
     static const int v = env_seg("KH_L1F_WPC", 0);
     if (v > 0) return (uint32_t)v;
     const size_t lds = lds_scatter_l1f(P, false, L1_THREADS * l1f_rpt());
-    const size_t regs = (l1f_rpt() == 8 ? L1F_WAVES_PER_EU : 4) * 4 / (L1_THREADS / 64);
+    const size_t regs = L1F_WAVES_PER_EU * 4 / (L1_THREADS / 64);
     return (uint32_t)std::max<size_t>(1, std::min<size_t>(regs, 163840 / lds));
 }
 static bool use_own_filter(const Graph *g);
@@ -341,21 +342,15 @@ static bool l1f_tw(const Src &src, int kpt) {
 }
 template <class Src>
 static L1FFn<Src> l1f_kernel(int kpt, int rpt, bool tw = false) {
-    if (tw && rpt == 8) {
-        switch (kpt) {
-            case 1: return k_scatter_l1f<Src, 1, 8, true>;
-            case 2: return k_scatter_l1f<Src, 2, 8, true>;
-            case 4: return k_scatter_l1f<Src, 4, 8, true>;
-            default: return k_scatter_l1f<Src, 8, 8, true>;
-        }
-    }
-    if (rpt == 16) {
-        switch (kpt) {
-            case 1: return k_scatter_l1f<Src, 1, 16>;
-            case 2: return k_scatter_l1f<Src, 2, 16>;
-            case 4: return k_scatter_l1f<Src, 4, 16>;
-            case 8: return k_scatter_l1f<Src, 8, 16>;
-            default: return k_scatter_l1f<Src, 16, 16>;
+    (void)rpt;
+    if constexpr (std::is_same<Src, SrcTwoBit>::value) {
+        if (tw) {
+            switch (kpt) {
+                case 1: return k_scatter_l1f<Src, 1, 8, true>;
+                case 2: return k_scatter_l1f<Src, 2, 8, true>;
+                case 4: return k_scatter_l1f<Src, 4, 8, true>;
+                default: return k_scatter_l1f<Src, 8, 8, true>;
+            }
         }
     }
     switch (kpt) {
@@ -371,20 +366,21 @@ static L1FFn<Src> l1f_kernel(int kpt, int rpt, bool tw = false) {
 static uint64_t bkt_plan(Graph *g, uint64_t nkmers) {
     Workspace &w = g->ws;
     const Params &P = g->prm;
-    if (w.bkt_base && w.bkt_nkmers == nkmers) return w.bkt_total;
+    if (w.bkt_base && w.bkt_nkmers == nkmers && w.bkt_sigma == g->cap_sigma) return w.bkt_total;
     const uint64_t F1 = P.F1, span = 1ull << (P.s0 + P.s2);
     const uint64_t slack = (uint64_t)l1f_workgroups(g, nkmers) * (1ull << l1f_blk_sh()) + 16;
     std::vector<uint64_t> base(F1 + 1, 0);
     uint64_t acc = 0;
-    int i = 0;
     for (uint64_t b = 0; b < F1; b++) {
         base[b] = acc;
-        const uint64_t lo = b * span;
-        while (i + 1 < P.n && lo >= P.tbase[i + 1]) i++;
-        if (lo >= P.tbase[i] + P.lsz[i]) continue;
-        const uint64_t nb = std::min<uint64_t>(span, P.tbase[i] + P.lsz[i] - lo);
-        const double mean = (double)nkmers * (double)nb / (double)P.p[i];
-        const uint64_t c = (uint64_t)(mean + 8.0 * sqrt(mean)) + slack;
+        const uint64_t lo = b * span, hi = lo + span;
+        double mean = 0;   // a paired bucket may hold the end of one table and the start of the next
+        for (int i = 0; i < P.n; i++) {
+            const uint64_t a = std::max(lo, P.tbase[i]), e = std::min(hi, P.tbase[i] + P.lsz[i]);
+            if (e > a) mean += (double)nkmers * (double)(e - a) / (double)P.p[i];
+        }
+        if (mean == 0) continue;
+        const uint64_t c = (uint64_t)(mean + g->cap_sigma * sqrt(mean)) + slack;
         acc += (c + 15) & ~15ull;
     }
     base[F1] = acc;
@@ -396,6 +392,7 @@ static uint64_t bkt_plan(Graph *g, uint64_t nkmers) {
     ensure((void **)&w.bkt_cur, &cap, F1 + 1, 8);
     KH_HIP(hipMemcpy(w.bkt_base, base.data(), (F1 + 1) * 8, hipMemcpyHostToDevice));
     w.bkt_nkmers = nkmers;
+    w.bkt_sigma = g->cap_sigma;
     w.bkt_total = acc;
     return acc;
 }
@@ -553,30 +550,17 @@ static size_t lds_scatter_l1(const Params &P, bool window, int tile_kmers) {
 
 constexpr int L2_SEG = 16;   // 128-B level-2 write segments
 constexpr int L2_RPT = 8;    // level-2 records per thread per tile
-static int l2_seg() { return env_seg("KH_L2_SEG", L2_SEG); }
-static int w_seg() { return env_seg("KH_W_SEG", 2); }   // measured: 8 -> 26.8, 2 -> 25.5 ms/step
+static int l2_seg() { return L2_SEG; }
+static int w_seg() { return 2; }   // winner tails of 2 (measured: 8 -> 26.8, 2 -> 25.5 ms/step, round 1)
 static size_t lds_scatter_l2(const Params &P) {
     const size_t F2 = (size_t)1 << P.s2;
     return F2 * 8 + F2 * 8 * l2_seg() + F2 * 4 + 8 + ((F2 + 1) & ~(size_t)1) * 2 + F2;
 }
 using L2Fn = void (*)(uint32_t, int, int, const uint64_t *, const uint32_t *, const uint64_t *, const uint64_t *,
                       uint64_t *);
-static L2Fn l2_kernel() {
-    switch (l2_seg()) {
-        case 2: return k_scatter_l2<PT_THREADS, 2, L2_RPT>;
-        case 4: return k_scatter_l2<PT_THREADS, 4, L2_RPT>;
-        case 8: return k_scatter_l2<PT_THREADS, 8, L2_RPT>;
-        default: return k_scatter_l2<PT_THREADS, 16, L2_RPT>;
-    }
-}
+static L2Fn l2_kernel() { return k_scatter_l2<PT_THREADS, L2_SEG, L2_RPT>; }
 using WFn = void (*)(Params, ApplyArgs, int, uint32_t, uint32_t, const uint64_t *, uint32_t *);
-static WFn w_kernel() {
-    switch (w_seg()) {
-        case 2: return k_scatter_w<PT_THREADS, 2>;
-        case 4: return k_scatter_w<PT_THREADS, 4>;
-        default: return k_scatter_w<PT_THREADS, 8>;
-    }
-}
+static WFn w_kernel() { return k_scatter_w<PT_THREADS, 2>; }
 static size_t lds_scatter_w(uint32_t FJ) {
     const size_t FJa = (FJ + 3) & ~3u;
     return W_RPC * 8 + (W_RPC + 4) * 4 + FJa * 8 + (size_t)PT_TILE * 4 + FJa * 4 * w_seg() + FJa * 4 * 2 + 64 + FJa;
@@ -652,6 +636,24 @@ static uint64_t own_filter(Graph *g, const Src &src, uint64_t nkmers, bool windo
     }
 }
 
+// Would the record buffers of a pass of nkmers k-mers, planned with capacity
+// margin `sigma`, fit in the device memory left (the current buffers are
+// freed and reallocated)?  Estimate: the expected records plus the margin
+// over every region, twice (level-1 and level-2 buffers, 8 B a record).
+static bool recs_fit(Graph *g, uint64_t nkmers, double sigma) {
+    const Params &P = g->prm;
+    const double R = (double)(1ull << P.s0);
+    double recs = 0;
+    for (int i = 0; i < P.n; i++) {
+        const double regions = (double)P.lsz[i] / R, mean = (double)nkmers * R / (double)P.p[i];
+        recs += regions * (mean + sigma * sqrt(mean) + (double)((l2f_parts(P.F1) + 1) << l2f_blk_sh()));
+    }
+    size_t freeb = 0, total = 0;
+    if (hipMemGetInfo(&freeb, &total) != hipSuccess) return false;
+    const double have = (double)freeb + 16.0 * (double)g->ws.cap_recs;
+    return 16.0 * recs * 1.05 < have * 0.95;
+}
+
 // ---------------------------------------------------------------------------
 // one device pass over a batch of <= 2^32 - 16 k-mers
 // A pass runs in three stages so a sharded group can exchange data between
@@ -664,11 +666,72 @@ struct PassState {
     bool bigc = false;
     ApplyArgs A;
     uint32_t *win = nullptr, *wout = nullptr;
+    // coarse-window winner path
+    bool coarse = false;
+    uint32_t ncw = 0, fpc = 0;
 };
+
+// The coarse-window winner path (k_apply_count with A.coarse, k_hist_wf,
+// k_scatter_wf, k_mark_wf) for unsharded Byte/Nibble passes; KH_WINNERS=1
+// keeps the per-region winner lists (development; sharded groups always do,
+// their windows are routed across ranks)
+static bool coarse_winners(const Graph *g) {
+    static const bool off = env_seg("KH_WINNERS", 0) == 1;
+    return !off && g->world == 1 && !g->grouped && g->kind != BIT;
+}
+
+// coarse-window runs -> fine windows: the windows' counts (one small copy),
+// chunks of WF_CHUNK winners per coarse window, a [coarse][fine][chunk] count
+// matrix (one extra zero entry: its scan's last value is the total), then
+// the 64-way scatter into the fine windows' contiguous ranges of wout
+static void winners_fine(Graph *g, PassState &ps) {
+    Workspace &w = g->ws;
+    hipStream_t st = g->stream;
+    const ApplyArgs &A = ps.A;
+    std::vector<unsigned long long> cur(MAX_CW), base(MAX_CW, 0);
+    KH_HIP(hipMemcpyAsync(cur.data(), w.cw_cur, MAX_CW * 8, hipMemcpyDeviceToHost, st));
+    KH_HIP(hipStreamSynchronize(st));
+    uint64_t acc = 0;
+    for (uint32_t c = 0; c < ps.ncw; c++) {
+        base[c] = acc;
+        acc += std::min<uint64_t>(1ull << A.cjs, ps.nkmers - ((uint64_t)c << A.cjs)) * (uint64_t)g->prm.n;
+    }
+    std::vector<WChunk> ch;
+    std::vector<uint64_t> cmbase(MAX_CW + 1, 0);
+    std::vector<uint32_t> cnk(MAX_CW, 0);
+    uint64_t m = 0;
+    for (uint32_t c = 0; c < ps.ncw; c++) {
+        const uint64_t n = cur[c] - base[c];
+        const uint32_t nk = (uint32_t)((n + WF_CHUNK - 1) / WF_CHUNK);
+        cmbase[c] = m;
+        cnk[c] = nk;
+        for (uint32_t k = 0; k < nk; k++)
+            ch.push_back(WChunk{base[c] + (uint64_t)k * WF_CHUNK, std::min<uint64_t>(cur[c], base[c] + (uint64_t)(k + 1) * WF_CHUNK),
+                                m, k, nk});
+        m += (uint64_t)nk * ps.fpc;
+    }
+    for (uint32_t c = ps.ncw; c <= MAX_CW; c++) cmbase[c] = m;
+    ensure(&w.wch, &w.cap_wch, std::max<size_t>(ch.size(), 1), sizeof(WChunk));
+    ensure((void **)&w.mcnt, &w.cap_m, m + 1, 4);
+    ensure((void **)&w.moff, &w.cap_moff, m + 1, 8);
+    if (!ch.empty()) KH_HIP(hipMemcpyAsync(w.wch, ch.data(), ch.size() * sizeof(WChunk), hipMemcpyHostToDevice, st));
+    KH_HIP(hipMemcpyAsync(w.cmbase, cmbase.data(), (MAX_CW + 1) * 8, hipMemcpyHostToDevice, st));
+    KH_HIP(hipMemcpyAsync(w.cnk, cnk.data(), MAX_CW * 4, hipMemcpyHostToDevice, st));
+    KH_HIP(hipMemsetAsync(w.mcnt + m, 0, 4, st));
+    const int js = ps.q.js;
+    if (!ch.empty())
+        TIMED("hist_w", hipLaunchKernelGGL(k_hist_wf, dim3((unsigned)ch.size()), dim3(WF_THREADS), 0, st, A.wco,
+                                           (const WChunk *)w.wch, js, ps.fpc, w.mcnt));
+    TIMED("scan", scan_counts(g, w.mcnt, w.moff, m + 1));
+    if (!ch.empty())
+        TIMED("scatter_w", hipLaunchKernelGGL(k_scatter_wf, dim3((unsigned)ch.size()), dim3(WF_THREADS), 0, st, A.wco,
+                                              (const WChunk *)w.wch, js, ps.fpc, w.moff, ps.wout));
+    KH_HIP(hipGetLastError());
+}
 
 template <class Src>
 static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
-    if (nkmers > MAX_PASS_KMERS) fail(KH_EVALUE, "device batch too large (more than 2560 * 2^20 k-mers)");
+    if (nkmers > MAX_PASS_KMERS) fail(KH_EVALUE, "device batch too large (more than 3200 * 2^20 k-mers)");
     const Params &P = g->prm;
     PassState ps;
     ps.q = pass_geo(P, nkmers);
@@ -687,7 +750,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     const uint64_t flag_bytes = (nkmers + 15) & ~15ull;
 
     const bool l2f_try = l2f_wanted(g, nkmers);
-    const uint64_t cap2 = l2f_try ? reg_plan(g, nkmers) : 0;   // level-2 capacity (records)
+    uint64_t cap2 = l2f_try ? reg_plan(g, nkmers) : 0;   // level-2 capacity (records)
     KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
     if (bigc) {
         KH_HIP(hipMemsetAsync(w.fullf, 0, flag_bytes, st));
@@ -797,18 +860,25 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
             const bool bkt = l1f || ownf;   // level 1 went into fixed-capacity buckets
             const uint64_t *bs = bkt ? w.bkt_base : w.off1;
             const uint64_t *be = bkt ? w.bkt_cur : w.off1 + 1;
-            static const int l2rpt = env_seg("KH_L2_RPT", L2_RPT);   // development: 8 or 16
-            TIMED("scatter_l2", hipLaunchKernelGGL((l2rpt == 16 ? k_scatter_l2f<PT_THREADS, 16> : k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(F1 * parts)),
+            TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(F1 * parts)),
                                                    dim3(PT_THREADS), lds_scatter_l2f(P), st, (uint32_t)F1, P.s0, P.s2,
                                                    parts, bs, be, w.reg_base, (unsigned long long *)w.reg_cur, w.rec1,
                                                    w.rec2, w.ctr, l2f_blk_sh()));
             uint64_t err = 0;
             KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
             KH_HIP(hipStreamSynchronize(st));
-            if (err & 12) {   // a bucket or region overflowed: redo the pass exactly
+            if (err & 12) {   // a bucket or region overflowed (the tables are untouched until apply)
+                KH_HIP(hipMemsetAsync(w.ctr + CTR_ERR, 0, 8, st));
+                // redo the pass on the fast path with 3x the capacity margin
+                // while the larger record buffers fit the device; beyond that,
+                // exactly (histogram path), and the next 8 passes too
+                if (g->cap_sigma < 72.0 && recs_fit(g, nkmers, g->cap_sigma * 3.0)) {
+                    g->cap_sigma *= 3.0;
+                    cap2 = reg_plan(g, nkmers);
+                    continue;
+                }
                 fast = false;
                 g->l2_cool = 8;
-                KH_HIP(hipMemsetAsync(w.ctr + CTR_ERR, 0, 8, st));
                 continue;
             }
         } else {
@@ -845,6 +915,32 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     A.rprefix[0] = 0;
     for (int i = 0; i < P.n; i++)
         A.rprefix[i + 1] = A.rprefix[i] + ((P.lsz[i] + (1ull << P.s0) - 1) >> P.s0);
+    // coarse windows of 2^cjs k-mers (<= 64), each a fine window multiple;
+    // window c may hold (its k-mers) x (tables) winners, the capacity of its
+    // range of the winner array (the dead level-1 records)
+    ps.coarse = coarse_winners(g);
+    A.coarse = ps.coarse ? 1 : 0;
+    A.cjs = std::max(q.js, ceil_log2(nkmers) - 6);
+    A.wco = win;
+    A.cw_cur = nullptr;
+    if (ps.coarse) {
+        ps.ncw = (uint32_t)((nkmers + (1ull << A.cjs) - 1) >> A.cjs);
+        ps.fpc = 1u << (A.cjs - q.js);
+        if (!w.cw_cur) {
+            KH_HIP(hipMalloc((void **)&w.cw_cur, MAX_CW * 8));
+            KH_HIP(hipMalloc((void **)&w.cmbase, (MAX_CW + 1) * 8));
+            KH_HIP(hipMalloc((void **)&w.cnk, MAX_CW * 4));
+        }
+        std::vector<unsigned long long> cb(MAX_CW, 0);
+        uint64_t acc = 0;
+        for (uint32_t c = 0; c < ps.ncw; c++) {
+            cb[c] = acc;
+            acc += std::min<uint64_t>(1ull << A.cjs, nkmers - ((uint64_t)c << A.cjs)) * (uint64_t)P.n;
+        }
+        if (acc > w.cap_recs) fail(KH_EDEVICE, "winner capacity exceeds the record buffer");
+        KH_HIP(hipMemcpyAsync(w.cw_cur, cb.data(), MAX_CW * 8, hipMemcpyHostToDevice, st));
+        A.cw_cur = w.cw_cur;
+    }
     const unsigned agrid = (unsigned)std::min<uint64_t>(q.regions, 256 * 2);
     if (P.kind == BIT)
         TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P), st, P, A));
@@ -858,6 +954,10 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
         TIMED("crossing", hipLaunchKernelGGL(k_crossing, dim3(1024), dim3(256), 0, st, P, w.rec2, w.xseg, wout,
                                              w.ctr, w.fullf));
 
+    if (ps.coarse) {
+        winners_fine(g, ps);
+        return ps;
+    }
     // winners -> k-mer windows
     const size_t wmeta = W_RPC * 8 + (W_RPC + 4) * 4;
     TIMED("hist_w", hipLaunchKernelGGL(k_hist_w, dim3(q.nchw), dim3(PT_THREADS), wmeta + (size_t)q.FJ * 4, st, P, A,
@@ -873,6 +973,12 @@ static void pass_mark_local(Graph *g, PassState &ps, bool want_new) {
     Workspace &w = g->ws;
     const PassGeo &q = ps.q;
     hipStream_t st = g->stream;
+    if (ps.coarse) {
+        TIMED("mark", hipLaunchKernelGGL(k_mark_wf, dim3(q.FJ), dim3(PT_THREADS), ((size_t)1 << q.js) / 8, st, ps.wout,
+                                         w.moff, w.cmbase, w.cnk, ps.fpc, q.js, w.ctr,
+                                         want_new ? w.newbits : nullptr));
+        return;
+    }
     TIMED("mark", hipLaunchKernelGGL(k_mark, dim3(q.FJ), dim3(PT_THREADS), ((size_t)1 << q.js) / 8, st, ps.wout,
                                      w.moff, w.mcnt, q.nchw, q.FJ, q.js, w.ctr, want_new ? w.newbits : nullptr));
 }
@@ -1320,12 +1426,19 @@ void engine_median_fixed_device(Graph *g, const void *d_reads, uint64_t nreads, 
     engine_sync_bigcounts(g);
     const unsigned grid = (unsigned)std::min<uint64_t>((nreads + 3) / 4, 8192);
     if (g->hash == MURMUR) {
-        const uint8_t *rd = padded_bytes(g, (const uint8_t *)d_reads, nreads * read_len);
-        SrcBytes s = src_bytes(g, rd, nullptr, nreads, kpr, nreads * read_len);
-        set_fixed(s, kpr);
-        TIMED("median", hipLaunchKernelGGL(k_median_fixed<SrcBytes>, dim3(grid), dim3(256), 0, g->stream, g->prm, s,
-                                           nreads, (uint32_t)kpr, g->d_tab, g->d_bc_keys, g->d_bc_vals, g->d_bc_n,
-                                           d_med, d_avg, d_sd));
+        // pieces of at most 2^24 reads: each builds its own reverse-complement
+        // stream, so the workspace stays bounded for any number of reads
+        const uint64_t cr = 1ull << 24;
+        for (uint64_t r0 = 0; r0 < nreads; r0 += cr) {
+            const uint64_t n = std::min(cr, nreads - r0);
+            const uint8_t *rd = padded_bytes(g, (const uint8_t *)d_reads + r0 * read_len, n * read_len);
+            SrcBytes s = src_bytes(g, rd, nullptr, n, kpr, n * read_len);
+            set_fixed(s, kpr);
+            const unsigned gr = (unsigned)std::min<uint64_t>((n + 3) / 4, 8192);
+            TIMED("median", hipLaunchKernelGGL(k_median_fixed<SrcBytes>, dim3(gr), dim3(256), 0, g->stream, g->prm,
+                                               s, n, (uint32_t)kpr, g->d_tab, g->d_bc_keys, g->d_bc_vals, g->d_bc_n,
+                                               d_med + r0, d_avg + r0, d_sd + r0));
+        }
     } else {
         SrcTwoBit s = src_twobit(g, (const uint64_t *)d_reads);
         set_fixed(s, kpr);
@@ -1341,9 +1454,18 @@ void engine_median_fixed_device(Graph *g, const void *d_reads, uint64_t nreads, 
 void engine_consume_bytes_fixed(Graph *g, const uint8_t *d_bytes, uint64_t nreads, uint64_t read_len) {
     if (read_len < (uint64_t)g->k) fail(KH_EVALUE, "reads shorter than k");
     const uint64_t kpr = read_len - g->k + 1;
-    d_bytes = padded_bytes(g, d_bytes, nreads * read_len);
-    consume_reads(g, src_bytes(g, d_bytes, nullptr, nreads, kpr, nreads * read_len), nullptr, nreads, nreads * kpr, kpr,
-                  nullptr);
+    // pieces of at most one device pass: the reverse-complement stream
+    // (src_bytes) is built per piece, so its workspace stays bounded for any
+    // number of reads; passes run in stream order, so the result is the
+    // whole stream's
+    uint64_t cr = std::max<uint64_t>(1, std::min<uint64_t>(g->batch_kmers, MAX_PASS_KMERS) / kpr);
+    const uint64_t np = (nreads + cr - 1) / std::max<uint64_t>(cr, 1);
+    if (np) cr = (nreads + np - 1) / np;   // equal pieces
+    for (uint64_t r0 = 0; r0 < nreads; r0 += cr) {
+        const uint64_t n = std::min(cr, nreads - r0);
+        const uint8_t *d = padded_bytes(g, d_bytes + r0 * read_len, n * read_len);
+        consume_reads(g, src_bytes(g, d, nullptr, n, kpr, n * read_len), nullptr, n, n * kpr, kpr, nullptr);
+    }
 }
 
 void engine_unpack_ascii(int device, const uint64_t *d_words, uint64_t nbases, uint8_t *d_bytes) {
@@ -1451,19 +1573,14 @@ static void set_lds_limits() {
             KH_LDS_MAX(l1_kernel<SrcBytes>(seg, kpt));
             KH_LDS_MAX(l1_kernel<SrcHashes>(seg, kpt));
         }
-    KH_LDS_MAX((k_scatter_l2<PT_THREADS, 2, L2_RPT>));
-    KH_LDS_MAX((k_scatter_l2f<PT_THREADS, 16>));
-    KH_LDS_MAX((k_scatter_l2<PT_THREADS, 4, L2_RPT>));
-    KH_LDS_MAX((k_scatter_l2<PT_THREADS, 8, L2_RPT>));
-    KH_LDS_MAX((k_scatter_l2<PT_THREADS, 16, L2_RPT>));
+    KH_LDS_MAX((k_scatter_l2<PT_THREADS, L2_SEG, L2_RPT>));
     KH_LDS_MAX((k_scatter_l2f<PT_THREADS, L2_RPT>));
-    for (int kpt : {1, 2, 4, 8, 16})
-        for (int rpt : {8, 16}) {
-            KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt, rpt));
-            KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt, rpt, true));
-            KH_LDS_MAX(l1f_kernel<SrcBytes>(kpt, rpt));
-            KH_LDS_MAX(l1f_kernel<SrcHashes>(kpt, rpt));
-        }
+    for (int kpt : {1, 2, 4, 8}) {
+        KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt, 8));
+        KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt, 8, true));
+        KH_LDS_MAX(l1f_kernel<SrcBytes>(kpt, 8));
+        KH_LDS_MAX(l1f_kernel<SrcHashes>(kpt, 8));
+    }
     KH_LDS_MAX((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>));
     for (int kpt : {1, 2, 4, 8}) {
         KH_LDS_MAX(own_l1f_kernel<SrcTwoBit>(kpt, false));
@@ -1487,10 +1604,9 @@ static void set_lds_limits() {
     KH_LDS_MAX((k_own_filter<SrcHashes, 8>));
     KH_LDS_MAX((k_own_filter<SrcHashes, 16>));
     KH_LDS_MAX((k_scatter_w<PT_THREADS, 2>));
-    KH_LDS_MAX((k_scatter_w<PT_THREADS, 4>));
-    KH_LDS_MAX((k_scatter_w<PT_THREADS, 8>));
 #undef KH_LDS_MAX
     (void)hipFuncSetAttribute((const void *)k_mark, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_mark_wf, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipGetLastError();
 }
 
@@ -1551,7 +1667,8 @@ Graph::~Graph() {
     Workspace &w = ws;
     void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.fullf, w.newbits, w.bc, w.bcn, w.bck, w.bcv,
                     w.off1, w.ch2, w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.xseg, w.reg_base, w.reg_cur, w.bkt_base, w.bkt_cur, w.ctr, w.d_words, w.d_koff, w.d_bytes,
-                    w.q_hashes, w.q_counts, w.frec, w.fcount, w.d_rbytes, w.sm_flags, w.sm_hash};
+                    w.q_hashes, w.q_counts, w.frec, w.fcount, w.d_rbytes, w.sm_flags, w.sm_hash, w.cw_cur, w.cmbase,
+                    w.cnk, w.wch};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (w.h_ctr) (void)hipHostFree(w.h_ctr);
@@ -1709,8 +1826,10 @@ ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n
     G->world = world;
     G->nlocal = nlocal;
     G->rank0 = nlocal == world ? 0 : rank;
-    for (int l = 0; l < nlocal; l++)
+    for (int l = 0; l < nlocal; l++) {
         G->shards.push_back(graph_create_shard(kind, hash, k, sizes, n, devices[l], world, G->rank0 + l));
+        G->shards.back()->grouped = true;
+    }
     G->loc.resize(nlocal);
     if (nlocal == 1 && world > 1) {
         if (!uid) fail(KH_EVALUE, "an RCCL group needs the unique id of rank 0");
@@ -1736,6 +1855,7 @@ ShardGroup *group_create_hosted(int kind, int hash, int k, const uint64_t *sizes
     G->hosted = true;
     G->tp = *t;
     G->shards.push_back(graph_create_shard(kind, hash, k, sizes, n, device, world, rank));
+    G->shards.back()->grouped = true;
     G->loc.resize(1);
     KH_HIP(hipSetDevice(device));
     KH_HIP(hipMalloc((void **)&G->d_red, 256 * 8));

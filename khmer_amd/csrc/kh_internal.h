@@ -50,10 +50,11 @@ struct DevBuf {
 };
 
 constexpr int MAXT = 32;  // tables per graph on device (NibbleStorage's own cap, storage.hh:290)
-// k-mers of one device pass: at most 2560 winner windows of 2^20 k-mers (the
-// LDS of k_scatter_w's per-window tails and k_mark's 2^20-bit bitmap); batch
-// k-mer indices stay 32-bit
-constexpr uint64_t MAX_PASS_KMERS = 2560ull << 20;
+// k-mers of one device pass: at most 3200 winner windows of 2^20 k-mers (the
+// LDS of k_scatter_w's per-window tails, ~115 KB, and k_mark's 2^20-bit
+// bitmap); batch k-mer indices stay 32-bit (3200 * 2^20 < 2^32 - 1 = NO_J).
+// The C2 step (6.5e9 k-mers) runs as two passes of 3.25e9.
+constexpr uint64_t MAX_PASS_KMERS = 3200ull << 20;
 
 // ---- partition geometry -----------------------------------------------------
 // Every table bin gets a global id G = tbase[i] + bin.  Regions are 2^s0 bins
@@ -108,12 +109,19 @@ struct Workspace {
     uint64_t *moff = nullptr;        // its exclusive scan
     void *scan_tmp = nullptr;        // rocPRIM scan temporary storage
     uint32_t *wcnt = nullptr;        // [regions] winners per region
+    // coarse-window winner path (unsharded passes; kh_apply.cuh k_*_wf)
+    unsigned long long *cw_cur = nullptr;   // [64] append cursors
+    uint64_t *cmbase = nullptr;              // [65] count-matrix base per coarse window
+    uint32_t *cnk = nullptr;                 // [64] chunks per coarse window
+    void *wch = nullptr;                     // WChunk descriptors
+    uint64_t cap_wch = 0;
     uint64_t cap_m = 0, cap_moff = 0, cap_scan = 0, cap_newbits = 0, cap_wcnt = 0;
     uint4 *xseg = nullptr;           // crossing-bin segments, one per region with crossings
     // fixed-capacity level 2 (k_scatter_l2f): region g holds [reg_base[g], reg_cur[g])
     uint64_t *reg_base = nullptr;    // [regions + 1] capacity prefix for passes of reg_nkmers k-mers
     uint64_t *reg_cur = nullptr;     // [regions] append cursors
     uint64_t cap_reg = 0, reg_nkmers = 0, reg_total = 0;
+    double reg_sigma = 0, bkt_sigma = 0;          // capacity margins the plans were made with
     // fixed-capacity level 1 (k_scatter_l1f): bucket b holds [bkt_base[b], bkt_cur[b])
     uint64_t *bkt_base = nullptr, *bkt_cur = nullptr;
     uint64_t bkt_nkmers = 0, bkt_total = 0;
@@ -143,6 +151,7 @@ struct Graph {
     // shard of a multi-GPU group: this graph holds bins [lo, lo + lsz) of every
     // table (lo = 0, lsz = sizes when not sharded); nbytes are the slice's bytes
     int world = 1, rank = 0;
+    bool grouped = false;             // a shard of a ShardGroup (its winners are routed by window)
     std::vector<uint64_t> lo, lsz;
     Geometry geo;
     Params prm;
@@ -160,6 +169,11 @@ struct Graph {
     std::unordered_set<uint64_t> tags;                  // hashgraph.hh:113 all_tags
     uint64_t batch_kmers = 1ull << 27;
     int l2_cool = 0;                  // passes left on the exact level 2 after a capacity overflow
+    // capacity margin of the fixed-capacity partition, in Poisson sigmas of
+    // each bucket's / region's expected record count; grown (x3, sticky) when
+    // a pass overflows -- skewed input (repeated k-mers) spreads region
+    // counts far wider than Poisson
+    double cap_sigma = 8.0;
     Workspace ws;
     // optional per-kernel HIP-event timing (kh_graph_set_profiling)
     bool profile = false;

@@ -589,15 +589,43 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
         PH(0);
         block_sync();
         PH(1);
+        // Block reservations are issued first (thread d owns bucket d and
+        // d + L1_THREADS; F1 <= 1024): the returned bases are needed only
+        // after the staging below, which hides the atomics' latency.
+        uint64_t rsv[2] = {0, 0};
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint32_t d = threadIdx.x + (uint32_t)u * L1_THREADS;
+            if (d < F1 && bcur[d] != DEAD) {
+                const uint32_t h = hist[d], L0 = cnt[d];
+                const uint32_t need = ((L0 + h + BLK - 1) >> blk_sh) - (((L0 + BLK - 1) & ~(BLK - 1)) >> blk_sh);
+                if (need) rsv[u] = atomicAdd(&bkt_cur[d], (unsigned long long)need * BLK);
+            }
+        }
         // stage region of bucket d: an even number of slots, a leading hole
         // when a record of the bucket is pending (its pair partner), the run,
-        // a trailing pad when the run ends unpaired
-        for (uint32_t d = threadIdx.x; d < F1; d += blockDim.x) {
-            const uint32_t h = hist[d];
-            lstart[d] = h ? (h + (cnt[d] & 1u) + 1u) & ~1u : 0u;
+        // a trailing pad when the run ends unpaired.  Region starts: padded
+        // run sizes and their exclusive scan by wave 0 alone (<= 16 buckets
+        // per lane), one barrier.
+        if (threadIdx.x < 64) {
+            const uint32_t lane = threadIdx.x, per = (F1 + 63) / 64, b0 = lane * per;
+            auto run = [&](uint32_t d) -> uint32_t {
+                const uint32_t h = hist[d];
+                return h ? (h + (cnt[d] & 1u) + 1u) & ~1u : 0u;
+            };
+            uint32_t sum = 0;
+            for (uint32_t t = 0; t < per && b0 + t < F1; t++) sum += run(b0 + t);
+            uint32_t incl = sum;
+            for (int dd = 1; dd < 64; dd <<= 1) {
+                const uint32_t y = __shfl_up(incl, dd, 64);
+                if (lane >= (uint32_t)dd) incl += y;
+            }
+            uint32_t acc = incl - sum;
+            for (uint32_t t = 0; t < per && b0 + t < F1; t++) {
+                lstart[b0 + t] = acc;
+                acc += run(b0 + t);
+            }
         }
-        block_sync();
-        block_scan_hist(lstart, lstart, F1, s_wtot);   // in place: region starts (even)
         block_sync();
         PH(2);
 #pragma unroll
@@ -625,10 +653,13 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
                 if (j < n1 && !(P.ablate & 32)) pend[a] = kmer_fetch(src, j);
             }
         }
-        // per bucket: block reservation (one atomic when the tile needs new
-        // blocks), the pending odd record when its pair completes, and the
-        // placement constants of this tile's run
-        for (uint32_t d = threadIdx.x; d < F1; d += blockDim.x) {
+        // per bucket: the reserved blocks (past the capacity: overflow), the
+        // pending odd record when its pair completes, and the placement
+        // constants of this tile's run
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint32_t d = threadIdx.x + (uint32_t)u * L1_THREADS;
+            if (d >= F1) continue;
             const uint32_t h = hist[d];
             if (!h && !last) continue;
             const uint32_t L0 = cnt[d];
@@ -638,7 +669,7 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             if (bc == DEAD) {
                 nb = DEAD;
             } else if (need) {
-                nb = atomicAdd(&bkt_cur[d], (unsigned long long)need * BLK);
+                nb = rsv[u];
                 if (nb + (uint64_t)need * BLK > bkt_base[d + 1]) {
                     atomicOr((unsigned long long *)&ctr[CTR_ERR], 8ull);
                     nb = DEAD;

@@ -104,6 +104,15 @@ class _ShardView(object):
         return bytes(buf[:n.value])
 
 
+def _read_mem(addr, n):
+    """n bytes at addr as bytes: ctypes.string_at takes a C int size, so
+    blocks over 2 GiB are read in pieces."""
+    piece = 1 << 30
+    if n <= piece:
+        return ctypes.string_at(addr, n)
+    return b"".join(ctypes.string_at(addr + a, min(piece, n - a)) for a in range(0, n, piece))
+
+
 _AG = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
 _BC = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int)
 _A2A = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
@@ -127,7 +136,9 @@ class HostTransport(object):
         world = rdv.world
 
         def failed(e):
+            import sys
             self.error = e
+            sys.stderr.write("khmer_amd host transport (rank %d): %r\n" % (rdv.rank, e))
             abort = getattr(rdv, "abort", None)
             if abort is not None:
                 try:
@@ -138,7 +149,7 @@ class HostTransport(object):
 
         def allgather(ctx, send, recv, nbytes):
             try:
-                parts = rdv.allgather(ctypes.string_at(send, nbytes) if nbytes else b"")
+                parts = rdv.allgather(_read_mem(send, nbytes) if nbytes else b"")
                 ctypes.memmove(recv, b"".join(parts), nbytes * world)
                 return 0
             except Exception as e:   # reported to the library as a failed collective
@@ -146,7 +157,7 @@ class HostTransport(object):
 
         def broadcast(ctx, buf, nbytes, root):
             try:
-                data = rdv.broadcast(ctypes.string_at(buf, nbytes) if rdv.rank == root else b"", root)
+                data = rdv.broadcast(_read_mem(buf, nbytes) if rdv.rank == root else b"", root)
                 if rdv.rank != root:
                     ctypes.memmove(buf, data, nbytes)
                 return 0
@@ -158,7 +169,7 @@ class HostTransport(object):
                 blocks, at = [], 0
                 for d in range(world):
                     n = send_bytes[d]
-                    blocks.append(ctypes.string_at(send + at, n) if n else b"")
+                    blocks.append(_read_mem(send + at, n) if n else b"")
                     at += n
                 got = rdv.alltoallv(blocks)
                 at = 0

@@ -13,6 +13,5 @@ run() {  # run <name> [ENV=VAL ...]
 }
 run base0 KH_NONE=0
 run s0_13 KH_S0=13
-run wseg4 KH_W_SEG=4
 run s2_9 KH_S2=9
 run base1 KH_NONE=0
