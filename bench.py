@@ -87,6 +87,8 @@ def parse():
                     help="feed k-mer offsets (variable-length read path) instead of the fixed-length path")
     ap.add_argument("--cpu-reads", type=int, default=1_000_000,
                     help="reads in the oracle CPU-baseline sample (0 = skip)")
+    ap.add_argument("--no-unprofiled", dest="unprofiled", action="store_false",
+                    help="skip the second, unprofiled run of the K steps (ms_per_step_unprofiled)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     a.graph, k, x = CONFIGS[a.config]
@@ -344,6 +346,18 @@ def main():
     elapsed = runner.max_over_ranks(t1 - t0)
     stats = runner.kernel_stats()
     runner.profile(False)
+    # the same K steps again without the per-kernel HIP events: how much the
+    # profiling in the timed region costs (reported, never `value`)
+    unprof = None
+    if args.unprofiled:
+        runner.barrier()
+        u0 = time.perf_counter()
+        for _ in range(args.steps):
+            runner.step()
+        runner.sync()
+        u1 = time.perf_counter()
+        runner.barrier()
+        unprof = runner.max_over_ranks(u1 - u0) * 1e3 / args.steps
     check_info = runner.check()
     # parity of the timed workload itself, when a golden fixture holds it
     fx = None if args.query else matching_fixture(args, nreads * world)
@@ -401,6 +415,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
+            "ms_per_step_unprofiled": unprof,
             "higher_is_better": True,
             "scaling": "strong" if (args.strong and world > 1) else "weak",
             "vs_baseline": None,

@@ -94,6 +94,22 @@ struct Prefetch {
     uint64_t v[APPLY_RECS];     // this thread's first records
 };
 
+// APPLY_RECS records per thread as APPLY_RECS / 2 16-B pairs: pair p0 + u * TH
+// + thread.  Records outside [e0, e1) (the odd ends of an unaligned region,
+// the pairs past its end) read as the ~0 sentinel.  One 16-B load per two
+// records: apply's record stream is bound by load instructions, not bytes.
+template <int TH>
+__device__ __forceinline__ void load_recs(const uint64_t *rec, uint64_t p0, uint64_t e0, uint64_t e1, uint64_t *v) {
+#pragma unroll
+    for (int u = 0; u < APPLY_RECS / 2; u++) {
+        const uint64_t r = 2 * (p0 + (uint64_t)u * TH + threadIdx.x);
+        ulonglong2 x = make_ulonglong2(~0ull, ~0ull);
+        if (r < e1) x = *(const ulonglong2 *)(rec + r);
+        v[2 * u] = r >= e0 ? x.x : ~0ull;
+        v[2 * u + 1] = r + 1 < e1 ? x.y : ~0ull;
+    }
+}
+
 template <int KIND, int TH = APPLY_THREADS>
 __device__ __forceinline__ void prefetch_region(const Params &P, const ApplyArgs &A, uint64_t rr, uint64_t total,
                                                 Bounds b, Prefetch &f) {
@@ -115,11 +131,7 @@ __device__ __forceinline__ void prefetch_region(const Params &P, const ApplyArgs
     } else {
         if (any && t < (f.ri.nb + 127) / 128) f.tv = ((const uint4 *)(tab + (f.ri.bin_lo >> 3)))[t];
     }
-#pragma unroll
-    for (int u = 0; u < APPLY_RECS; u++) {
-        const uint64_t q = f.ri.e0 + (uint64_t)u * TH + t;
-        f.v[u] = q < f.ri.e1 ? A.rec[q] : ~0ull;
-    }
+    load_recs<TH>(A.rec, f.ri.e0 >> 1, f.ri.e0, f.ri.e1, f.v);
 }
 
 // one record of a Byte/Nibble region: two independent fire-and-forget LDS
@@ -234,29 +246,18 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
         if (!(P.ablate & 2)) {
             // two batches of APPLY_RECS loads in flight: batch k+1 is issued
             // before batch k's atomics, so each wait is for the older batch only
-            const uint64_t step = (uint64_t)APPLY_RECS * TH;
+            const uint64_t step = (uint64_t)(APPLY_RECS / 2) * TH;   // pairs
+            const uint64_t pend = (ri.e1 + 1) >> 1;
             uint64_t va[APPLY_RECS], vb[APPLY_RECS];
-            uint64_t q0 = ri.e0 + step + t;
-#pragma unroll
-            for (int u = 0; u < APPLY_RECS; u++) {
-                const uint64_t q = q0 + (uint64_t)u * TH;
-                va[u] = q < ri.e1 ? A.rec[q] : ~0ull;
-            }
+            uint64_t q0 = (ri.e0 >> 1) + step;
+            load_recs<TH>(A.rec, q0, ri.e0, ri.e1, va);
 #pragma unroll
             for (int u = 0; u < APPLY_RECS; u++) count_record(cur.v[u], cnt, minj);
-            for (; q0 < ri.e1; q0 += 2 * step) {
-#pragma unroll
-                for (int u = 0; u < APPLY_RECS; u++) {
-                    const uint64_t q = q0 + step + (uint64_t)u * TH;
-                    vb[u] = q < ri.e1 ? A.rec[q] : ~0ull;
-                }
+            for (; q0 < pend; q0 += 2 * step) {
+                load_recs<TH>(A.rec, q0 + step, ri.e0, ri.e1, vb);
 #pragma unroll
                 for (int u = 0; u < APPLY_RECS; u++) count_record(va[u], cnt, minj);
-#pragma unroll
-                for (int u = 0; u < APPLY_RECS; u++) {
-                    const uint64_t q = q0 + 2 * step + (uint64_t)u * TH;
-                    va[u] = q < ri.e1 ? A.rec[q] : ~0ull;
-                }
+                load_recs<TH>(A.rec, q0 + 2 * step, ri.e0, ri.e1, va);
 #pragma unroll
                 for (int u = 0; u < APPLY_RECS; u++) count_record(vb[u], cnt, minj);
             }
@@ -500,29 +501,18 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyA
         if (t < 4) chg[t] = 0;
         block_sync();
         {
-            const uint64_t step = (uint64_t)APPLY_RECS * APPLY_THREADS;
+            const uint64_t step = (uint64_t)(APPLY_RECS / 2) * APPLY_THREADS;   // pairs
+            const uint64_t pend = (ri.e1 + 1) >> 1;
             uint64_t va[APPLY_RECS], vb[APPLY_RECS];
-            uint64_t q0 = ri.e0 + step + t;
-#pragma unroll
-            for (int u = 0; u < APPLY_RECS; u++) {
-                const uint64_t q = q0 + (uint64_t)u * APPLY_THREADS;
-                va[u] = q < ri.e1 ? A.rec[q] : ~0ull;
-            }
+            uint64_t q0 = (ri.e0 >> 1) + step;
+            load_recs<APPLY_THREADS>(A.rec, q0, ri.e0, ri.e1, va);
 #pragma unroll
             for (int u = 0; u < APPLY_RECS; u++) bit_record(cur.v[u], minj);
-            for (; q0 < ri.e1; q0 += 2 * step) {
-#pragma unroll
-                for (int u = 0; u < APPLY_RECS; u++) {
-                    const uint64_t q = q0 + step + (uint64_t)u * APPLY_THREADS;
-                    vb[u] = q < ri.e1 ? A.rec[q] : ~0ull;
-                }
+            for (; q0 < pend; q0 += 2 * step) {
+                load_recs<APPLY_THREADS>(A.rec, q0 + step, ri.e0, ri.e1, vb);
 #pragma unroll
                 for (int u = 0; u < APPLY_RECS; u++) bit_record(va[u], minj);
-#pragma unroll
-                for (int u = 0; u < APPLY_RECS; u++) {
-                    const uint64_t q = q0 + 2 * step + (uint64_t)u * APPLY_THREADS;
-                    va[u] = q < ri.e1 ? A.rec[q] : ~0ull;
-                }
+                load_recs<APPLY_THREADS>(A.rec, q0 + 2 * step, ri.e0, ri.e1, va);
 #pragma unroll
                 for (int u = 0; u < APPLY_RECS; u++) bit_record(vb[u], minj);
             }

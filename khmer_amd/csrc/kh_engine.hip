@@ -194,7 +194,6 @@ static uint32_t l2f_parts(uint32_t F1) {
     return std::max<uint32_t>(1, std::min<uint32_t>(32, (8192 + F1 - 1) / F1));
 }
 static size_t lds_scatter_l2f(const Params &P) { return ((size_t)1 << P.s2) * (8 + 8 + 16 * 8 + 4 + 4 + 2) + 16; }
-
 // The fixed-capacity path is used when a full region expects >= 512 records
 // per pass (the capacity slack is then a few percent); KH_L2_EXACT=1 forces
 // the histogram path (development).
@@ -861,9 +860,9 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
             const uint64_t *bs = bkt ? w.bkt_base : w.off1;
             const uint64_t *be = bkt ? w.bkt_cur : w.off1 + 1;
             TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(F1 * parts)),
-                                                   dim3(PT_THREADS), lds_scatter_l2f(P), st, (uint32_t)F1, P.s0, P.s2,
-                                                   parts, bs, be, w.reg_base, (unsigned long long *)w.reg_cur, w.rec1,
-                                                   w.rec2, w.ctr, l2f_blk_sh()));
+                                                   dim3(PT_THREADS), lds_scatter_l2f(P), st, (uint32_t)F1, P.s0,
+                                                   P.s2, parts, bs, be, w.reg_base, (unsigned long long *)w.reg_cur,
+                                                   w.rec1, w.rec2, w.ctr, l2f_blk_sh()));
             uint64_t err = 0;
             KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
             KH_HIP(hipStreamSynchronize(st));

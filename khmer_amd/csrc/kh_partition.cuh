@@ -1296,9 +1296,22 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
     if (__builtin_amdgcn_readfirstlane((uint32_t)ctr[CTR_ERR]) & 8u) return;
     const uint32_t b = blockIdx.x / parts, p = blockIdx.x % parts;
     const uint64_t b0 = bstart[b], b1 = min(bend[b], bstart[b + 1]);
-    const uint64_t len = (b1 - b0 + parts - 1) / parts;
+    // parts of an even length: every tile starts on a 16-B record pair
+    // (bucket bases are block-aligned), loaded with one 16-B load per pair
+    const uint64_t len = ((b1 - b0 + parts - 1) / parts + 1) & ~1ull;
     const uint64_t r0 = min(b1, b0 + (uint64_t)p * len), r1 = min(b1, r0 + len);
     const uint64_t gb = (uint64_t)b << s2;
+    auto load_tile = [&](uint64_t n0, uint64_t *v) {
+        const uint64_t n1 = min(r1, n0 + TILE);
+#pragma unroll
+        for (int q = 0; q < RPT / 2; q++) {
+            const uint64_t idx = n0 + 2 * ((uint64_t)q * THREADS + threadIdx.x);
+            ulonglong2 x = make_ulonglong2(~0ull, ~0ull);
+            if (idx < n1) x = *(const ulonglong2 *)(rec_in + idx);
+            v[2 * q] = x.x;
+            v[2 * q + 1] = idx + 1 < n1 ? x.y : ~0ull;
+        }
+    };
     const uint64_t rmask = (1ull << s0) - 1;
     for (uint32_t d = threadIdx.x; d < F2; d += THREADS) {
         bcur[d] = 0;
@@ -1313,11 +1326,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
         return nbase[d] == L2F_DEAD ? L2F_DEAD : nbase[d] + (L - split);
     };
     uint64_t v[RPT];
-#pragma unroll
-    for (int q = 0; q < RPT; q++) {
-        const uint64_t idx = r0 + (uint64_t)q * THREADS + threadIdx.x;
-        v[q] = idx < min(r1, r0 + TILE) ? rec_in[idx] : ~0ull;
-    }
+    load_tile(r0, v);
     PH_BEGIN(8);
     const uint32_t ntiles = uniform_u32((uint32_t)((r1 - r0 + TILE - 1) / TILE));
     for (uint32_t ti = 0; ti < ntiles; ti++) {
@@ -1333,14 +1342,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
             if (x[q] != ~0ull) rank[q] = atomicAdd(&hist[(uint32_t)x[q] >> s0], 1u);
         }
         PH(0);
-        {
-            const uint64_t n0 = t0 + TILE, n1 = min(r1, n0 + TILE);
-#pragma unroll
-            for (int q = 0; q < RPT; q++) {
-                const uint64_t idx = n0 + (uint64_t)q * THREADS + threadIdx.x;
-                v[q] = idx < n1 ? rec_in[idx] : ~0ull;
-            }
-        }
+        load_tile(t0 + TILE, v);
         block_sync();
         PH(1);
         // blocks for this tile (one reservation per region that needs any) and
