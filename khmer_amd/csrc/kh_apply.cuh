@@ -469,26 +469,34 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
 }
 
 // Bit storage (Bloom): BitStorage::test_and_set_bits (storage.hh:172-199)
-__global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyArgs A) {
+// TH threads over a region of 2^14 bins (BPT bins per thread).  Coarse-window
+// winners (A.coarse) are counting-sorted in LDS exactly as in k_apply_count,
+// staged in wst[] (BIT has no count array to reuse, so it has its own).
+template <int TH>
+__global__ void __launch_bounds__(TH, 4) k_apply_bit(Params P, ApplyArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int BPT = 32;               // 2^14 bins / 512 threads
+    constexpr int BPT = (1 << 14) / TH;
     const uint32_t R = 1u << P.s0;
     uint32_t *minj = (uint32_t *)smem;          // [R]
     uint32_t *chg = minj + R;                   // [4] changed 128-bin chunks
     uint32_t *s_wt = chg + 4;                   // [16]
     uint32_t *bits32 = s_wt + 16;               // [R/32]
     uint8_t *bits = (uint8_t *)bits32;
+    uint32_t *chist = bits32 + R / 32;          // [MAX_CW] coarse windows: counts, then cursors
+    uint32_t *cst0 = chist + MAX_CW;            // [MAX_CW] window's first staging slot
+    unsigned long long *cgb = (unsigned long long *)(cst0 + MAX_CW);   // [MAX_CW] window's output base
+    uint32_t *wst = (uint32_t *)(cgb + MAX_CW);   // [R] winners in window order (coarse only)
     const uint32_t t = threadIdx.x;
     uint64_t occ = 0;
     const uint64_t total = A.rprefix[P.n];
     Prefetch cur, nxt;
-    prefetch_region<BIT>(P, A, blockIdx.x, total, load_bounds(P, A, blockIdx.x, total), cur);
+    prefetch_region<BIT, TH>(P, A, blockIdx.x, total, load_bounds(P, A, blockIdx.x, total), cur);
     Bounds bnext = load_bounds(P, A, blockIdx.x + gridDim.x, total);
     for (uint64_t rr = blockIdx.x; rr < total; rr += gridDim.x) {
         const RegionInfo ri = cur.ri;
         if (ri.e0 == ri.e1) {
             if (t == 0) A.wcnt[rr] = 0;
-            prefetch_region<BIT>(P, A, rr + gridDim.x, total, bnext, cur);
+            prefetch_region<BIT, TH>(P, A, rr + gridDim.x, total, bnext, cur);
             bnext = load_bounds(P, A, rr + 2 * (uint64_t)gridDim.x, total);
             continue;
         }
@@ -499,49 +507,54 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyA
         if (t < nchunk) ((uint4 *)bits)[t] = cur.tv;
         for (uint32_t x = t; x < nchunk * 32; x += blockDim.x) ((uint4 *)minj)[x] = make_uint4(NO_J, NO_J, NO_J, NO_J);
         if (t < 4) chg[t] = 0;
+        if (t < MAX_CW) chist[t] = 0;
         block_sync();
         {
-            const uint64_t step = (uint64_t)(APPLY_RECS / 2) * APPLY_THREADS;   // pairs
+            const uint64_t step = (uint64_t)(APPLY_RECS / 2) * TH;   // pairs
             const uint64_t pend = (ri.e1 + 1) >> 1;
             uint64_t va[APPLY_RECS], vb[APPLY_RECS];
             uint64_t q0 = (ri.e0 >> 1) + step;
-            load_recs<APPLY_THREADS>(A.rec, q0, ri.e0, ri.e1, va);
+            load_recs<TH>(A.rec, q0, ri.e0, ri.e1, va);
 #pragma unroll
             for (int u = 0; u < APPLY_RECS; u++) bit_record(cur.v[u], minj);
             for (; q0 < pend; q0 += 2 * step) {
-                load_recs<APPLY_THREADS>(A.rec, q0 + step, ri.e0, ri.e1, vb);
+                load_recs<TH>(A.rec, q0 + step, ri.e0, ri.e1, vb);
 #pragma unroll
                 for (int u = 0; u < APPLY_RECS; u++) bit_record(va[u], minj);
-                load_recs<APPLY_THREADS>(A.rec, q0 + 2 * step, ri.e0, ri.e1, va);
+                load_recs<TH>(A.rec, q0 + 2 * step, ri.e0, ri.e1, va);
 #pragma unroll
                 for (int u = 0; u < APPLY_RECS; u++) bit_record(vb[u], minj);
             }
         }
         block_sync();
-        prefetch_region<BIT>(P, A, rr + gridDim.x, total, bnext, nxt);
+        prefetch_region<BIT, TH>(P, A, rr + gridDim.x, total, bnext, nxt);
         bnext = bafter;
-        // pass 1 (thread per bin): winners set their bit
+        // pass 1 (thread per bin): winners set their bit (and, coarse, count
+        // per window)
         uint32_t nw = 0;
         const uint32_t lane = t & 63;
+        const int cjs = A.cjs;
 #pragma unroll 2
         for (int u = 0; u < BPT; u++) {
-            const uint32_t o = t + (uint32_t)u * APPLY_THREADS;
+            const uint32_t o = t + (uint32_t)u * TH;
             bool win = false;
-            if (o < nb && minj[o] != NO_J) {
+            const uint32_t m = o < nb ? minj[o] : NO_J;
+            if (m != NO_J) {
                 if ((bits[o >> 3] >> (o & 7)) & 1) {   // bit already set: not new
                     minj[o] = NO_J;
                 } else {
                     win = true;
                     nw++;
                     occ += (ri.i == 0);
+                    if (A.coarse) atomicAdd(&chist[m >> cjs], 1u);
                 }
             }
             // a wave's 64 bins are two 32-bit words of the bit array and one
             // 128-bin write-back chunk
-            const uint64_t m = __ballot(win);
-            if (m) {
-                if (lane == 0 && (uint32_t)m) atomicOr(&bits32[o >> 5], (uint32_t)m);
-                if (lane == 32 && (uint32_t)(m >> 32)) atomicOr(&bits32[o >> 5], (uint32_t)(m >> 32));
+            const uint64_t bm = __ballot(win);
+            if (bm) {
+                if (lane == 0 && (uint32_t)bm) atomicOr(&bits32[o >> 5], (uint32_t)bm);
+                if (lane == 32 && (uint32_t)(bm >> 32)) atomicOr(&bits32[o >> 5], (uint32_t)(bm >> 32));
                 if (lane == 0) atomicOr(&chg[o >> 12], 1u << ((o >> 7) & 31));
             }
         }
@@ -552,15 +565,44 @@ __global__ void __launch_bounds__(APPLY_THREADS, 4) k_apply_bit(Params P, ApplyA
             if ((chg[x >> 5] >> (x & 31)) & 1) ((uint4 *)tab)[x] = ((const uint4 *)bits)[x];
         uint32_t wall;
         uint64_t pos = ri.e0 + winner_base(s_wt, &wall) + wex;
-        if (nw) {
+        if (t == 0) A.wcnt[rr] = wall;
+        if (A.coarse) {
+            if (t < 64) {
+                const uint32_t c = chist[t];
+                uint32_t incl = c;
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = __shfl_up(incl, d, 64);
+                    if (t >= (uint32_t)d) incl += y;
+                }
+                cst0[t] = incl - c;
+                cgb[t] = c ? atomicAdd(&A.cw_cur[t], (unsigned long long)c) : 0ull;
+                chist[t] = 0;   // placement cursors
+            }
+            block_sync();
+            if (nw) {
+#pragma unroll 2
+                for (int u = 0; u < BPT; u++) {
+                    const uint32_t o = t + (uint32_t)u * TH;
+                    const uint32_t m = o < nb ? minj[o] : NO_J;
+                    if (m != NO_J) {
+                        const uint32_t c = m >> cjs;
+                        wst[cst0[c] + atomicAdd(&chist[c], 1u)] = m;
+                    }
+                }
+            }
+            block_sync();
+            for (uint32_t x = t; x < wall; x += TH) {
+                const uint32_t v = wst[x], c = v >> cjs;
+                A.wco[cgb[c] + (x - cst0[c])] = v;
+            }
+        } else if (nw) {
 #pragma unroll 2
             for (int u = 0; u < BPT; u++) {
-                const uint32_t o = t + (uint32_t)u * APPLY_THREADS;
+                const uint32_t o = t + (uint32_t)u * TH;
                 const uint32_t m = o < nb ? minj[o] : NO_J;
                 if (m != NO_J) A.win[pos++] = m;
             }
         }
-        if (t == 0) A.wcnt[rr] = wall;
         block_sync();
         cur = nxt;
     }

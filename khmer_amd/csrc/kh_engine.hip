@@ -164,7 +164,17 @@ static void bcmap_merge(Graph *g, uint64_t nkeys, uint64_t n_ff) {
 static void ensure_recs(Graph *g, uint64_t recs) {
     Workspace &w = g->ws;
     if (recs <= w.cap_recs && w.rec1) return;
-    uint64_t cap = std::max<uint64_t>(recs, w.cap_recs + w.cap_recs / 2);
+    // grow by half (fewer reallocations) while that fits next to everything
+    // else on the device; the exact need otherwise
+    uint64_t grow = w.cap_recs + w.cap_recs / 2;
+    size_t freeb = 0, total = 0;
+    if (hipMemGetInfo(&freeb, &total) == hipSuccess) {
+        const double fit = ((double)freeb + 16.0 * (double)w.cap_recs) * 0.95 / 16.0 - 64.0;
+        grow = std::min<uint64_t>(grow, fit > 0 ? (uint64_t)fit : 0);
+    } else {
+        (void)hipGetLastError();
+    }
+    uint64_t cap = std::max<uint64_t>(recs, grow);
     cap = std::max<uint64_t>(cap, 1024);
     for (uint64_t **pp : {&w.rec1, &w.rec2}) {
         if (*pp) KH_HIP(hipFree(*pp));
@@ -574,9 +584,11 @@ static unsigned agrid_count(const Graph *g, const PassGeo &q) {
     const uint64_t per_cu = g->prm.s0 == 14 ? 1 : 2;
     return (unsigned)std::min<uint64_t>(q.regions, per_cu * device_cus(g));
 }
-static size_t lds_apply(const Params &P) {
+static size_t lds_apply(const Params &P, bool coarse = false) {
     const size_t R = (size_t)1 << P.s0;
-    return P.kind == BIT ? R * 4 + 16 + 64 + R / 8 : R * 4 * 2 + (R / 512) * 4 + 64 + R / 8 + 16 + R + R / 4;
+    if (P.kind == BIT)   // coarse-window winners: window arrays + a winner staging array
+        return R * 4 + 16 + 64 + R / 8 + (coarse ? MAX_CW * 16 + R * 4 : 0);
+    return R * 4 * 2 + (R / 512) * 4 + 64 + R / 8 + 16 + R + R / 4;
 }
 
 // A shard's level 1 through k_own_filter (kh_partition.cuh) when it owns a
@@ -676,7 +688,7 @@ struct PassState {
 // their windows are routed across ranks)
 static bool coarse_winners(const Graph *g) {
     static const bool off = env_seg("KH_WINNERS", 0) == 1;
-    return !off && g->world == 1 && !g->grouped && g->kind != BIT;
+    return !off && g->world == 1 && !g->grouped;
 }
 
 // coarse-window runs -> fine windows: the windows' counts (one small copy),
@@ -941,8 +953,12 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
         A.cw_cur = w.cw_cur;
     }
     const unsigned agrid = (unsigned)std::min<uint64_t>(q.regions, 256 * 2);
-    if (P.kind == BIT)
-        TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit, dim3(agrid), dim3(APPLY_THREADS), lds_apply(P), st, P, A));
+    if (P.kind == BIT && ps.coarse)   // one 1024-thread workgroup per CU (the staging array), else two of 512
+        TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit<1024>, dim3((unsigned)std::min<uint64_t>(q.regions, device_cus(g))),
+                                              dim3(1024), lds_apply(P, true), st, P, A));
+    else if (P.kind == BIT)
+        TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit<APPLY_THREADS>, dim3(agrid), dim3(APPLY_THREADS),
+                                              lds_apply(P), st, P, A));
     else if (P.kind == NIBBLE)
         TIMED("apply_nibble", hipLaunchKernelGGL(apply_count_kernel<NIBBLE>(P), dim3(agrid_count(g, q)),
                                                  dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
@@ -1564,7 +1580,8 @@ static void set_lds_limits() {
     (void)hipFuncSetAttribute((const void *)k_apply_count<BYTE, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               lim);
-    (void)hipFuncSetAttribute((const void *)k_apply_bit, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_bit<APPLY_THREADS>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_bit<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
 #define KH_LDS_MAX(...) (void)hipFuncSetAttribute((const void *)__VA_ARGS__, hipFuncAttributeMaxDynamicSharedMemorySize, lim)
     for (int kpt : {1, 2, 4, 8})
         for (bool seg : {false, true}) {

@@ -607,12 +607,29 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
         // a trailing pad when the run ends unpaired.  Region starts: padded
         // run sizes and their exclusive scan by wave 0 alone (<= 16 buckets
         // per lane), one barrier.
-        if (threadIdx.x < 64) {
+        auto run = [&](uint32_t d) -> uint32_t {
+            const uint32_t h = hist[d];
+            return h ? (h + (cnt[d] & 1u) + 1u) & ~1u : 0u;
+        };
+        if (F1 > 256) {
+            // many buckets: every thread scans two (F1 <= 2 * L1_THREADS),
+            // wave totals through s_wtot (one more barrier)
+            const uint32_t d0 = 2 * threadIdx.x;
+            const uint32_t r0 = d0 < F1 ? run(d0) : 0u, r1 = d0 + 1 < F1 ? run(d0 + 1) : 0u;
+            const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+            uint32_t incl = r0 + r1;
+            for (int dd = 1; dd < 64; dd <<= 1) {
+                const uint32_t y = __shfl_up(incl, dd, 64);
+                if (lane >= (uint32_t)dd) incl += y;
+            }
+            if (lane == 63) s_wtot[wave] = incl;
+            block_sync();
+            uint32_t acc = incl - r0 - r1;
+            for (uint32_t w = 0; w < wave; w++) acc += s_wtot[w];
+            if (d0 < F1) lstart[d0] = acc;
+            if (d0 + 1 < F1) lstart[d0 + 1] = acc + r0;
+        } else if (threadIdx.x < 64) {
             const uint32_t lane = threadIdx.x, per = (F1 + 63) / 64, b0 = lane * per;
-            auto run = [&](uint32_t d) -> uint32_t {
-                const uint32_t h = hist[d];
-                return h ? (h + (cnt[d] & 1u) + 1u) & ~1u : 0u;
-            };
             uint32_t sum = 0;
             for (uint32_t t = 0; t < per && b0 + t < F1; t++) sum += run(b0 + t);
             uint32_t incl = sum;
