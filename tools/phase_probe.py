@@ -13,18 +13,21 @@ from khmer_amd._lib import lib, check  # noqa: E402
 
 PHASES = {
     "scatter_l1 (exact)": (8, ["tile top", "hash+rank", "scan", "stage", "tails", "write"]),
-    "apply": (16, ["records", "pass-1 wait", "winner scan", "write-back", "pass 1", "init"]),
+    "apply": (16, ["init barrier", "records+barrier", "winner scan+barrier", "write-back+winners", "pass 1",
+                   "init"]),
     "scatter_l1f": (24, ["hash+rank", "barrier 1", "starts+scan", "stage", "reserve", "barrier 2", "write-out",
                          "advance+top barrier"]),
     "scatter_l2f": (32, ["wait+rank", "prefetch+barrier", "reserve+flist", "barrier", "flush", "barrier",
                          "stores", "advance+top barrier"]),
 }
 
+# usage: phase_probe.py [reads] [table size] [k]
 reads = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
-L, k = 150, 21
-g = khmer_amd.Countgraph(k, 1e9, 4)
+x = float(sys.argv[2]) if len(sys.argv) > 2 else 1e9
+L, k = 150, int(sys.argv[3]) if len(sys.argv) > 3 else 21
+g = khmer_amd.Countgraph(k, x, 4)
 g.set_use_bigcount(True)
-check(lib.kh_graph_set_batch_kmers(g._g, 2560 << 20))
+check(lib.kh_graph_set_batch_kmers(g._g, 3200 << 20))
 words, koff = ctypes.c_void_p(), ctypes.c_void_p()
 check(lib.kh_device_malloc(0, reads * L // 32 * 8 + 64, ctypes.byref(words)))
 check(lib.kh_device_malloc(0, (reads + 1) * 8, ctypes.byref(koff)))
