@@ -79,6 +79,9 @@ def parse():
                          "0 = iid uniform reads")
     ap.add_argument("--strong", action="store_true",
                     help="multi-GPU strong scaling: --reads is the whole job, split over the ranks")
+    ap.add_argument("--exchange", action="store_true",
+                    help="multi-GPU Option A: every rank hashes only its own reads and sends each level-1 bucket "
+                         "to its owner (default: Option B, read broadcast + owner-computes)")
     ap.add_argument("--query", action="store_true",
                     help="time get_median_count over the reads (tables built from them first, untimed)")
     ap.add_argument("--ablate", type=int, default=0,
@@ -123,7 +126,16 @@ def matching_fixture(args, total_reads):
     return None
 
 
-def compare_fixture(fx, n_unique, n_occupied, table_sha):
+def compare_fixture(fx, n_unique, n_occupied, table_sha, stream_order=True):
+    """stream_order=False (exchange mode: a pass-interleaved stream): the
+    tables and n_occupied do not depend on the order; n_unique does, so it is
+    not compared."""
+    if not stream_order:
+        out = {"fixture": fx["config"], "n_occupied_match": n_occupied == fx["n_occupied"],
+               "n_unique": "pass-interleaved stream (not the fixture's order): not compared"}
+        if table_sha is not None:
+            out["tables_match"] = list(table_sha) == list(fx["table_sha256"])
+        return out
     out = {"fixture": fx["config"], "counters_match": n_unique == fx["n_unique_kmers"] and
            n_occupied == fx["n_occupied"]}
     if table_sha is not None:
@@ -364,7 +376,8 @@ def main():
     if fx is not None:
         sha = runner.table_sha256()   # collective when sharded
         if rank == 0:
-            check_info.update(compare_fixture(fx, check_info["n_unique_kmers"], check_info["n_occupied"], sha))
+            check_info.update(compare_fixture(fx, check_info["n_unique_kmers"], check_info["n_occupied"], sha,
+                                              stream_order=not (args.exchange and world > 1)))
 
     bpk = query_bytes_per_kmer(L, k, nt) if args.query else algorithmic_bytes_per_kmer(L, k, nt)
     total_kmers = nkmers * world * args.steps
@@ -428,7 +441,7 @@ def main():
                 "k": k, "n_tables": nt, "table_sizes": sizes, "reads_per_gpu": nreads,
                 "read_len": L, "kmers_per_gpu_per_step": nkmers, "bigcount": args.bigcount,
                 "batch_kmers": args.batch_kmers,
-                "parallelism": ("shard%d" % world) if world > 1 else "single",
+                "parallelism": (("exchange%d" if args.exchange else "shard%d") % world) if world > 1 else "single",
                 "path": "get_median_count" if args.query else "consume",
                 "hash": "murmur3" if args.murmur else "twobit",
                 "genome": args.genome or None,

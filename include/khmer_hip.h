@@ -282,6 +282,24 @@ int kh_group_slice(kh_group *grp, int l, int table, uint64_t *lo, uint64_t *size
  * fixed-length reads: d_words[l] = local shard l's own reads (nlocal pointers) */
 int kh_group_consume_packed_fixed_device(kh_group *grp, const uint64_t *const *d_words, uint64_t nreads,
                                          uint64_t read_len);
+/* Group modes.  KH_GROUP_BROADCAST (kh_group_create): the
+ * slices above, every rank hashes every source's reads (Option B).
+ * KH_GROUP_EXCHANGE (Option A): every rank hashes only its own reads into the
+ * unsharded level-1 buckets and sends each bucket to its owner (grouped
+ * ncclSend/ncclRecv; host transport: alltoallv); rank r owns a contiguous
+ * range of level-1 buckets, i.e. bucket-aligned slices reported by
+ * kh_group_rank_slice.  A consume call's stream is taken pass by pass: pass p
+ * holds the p-th chunk of every rank's reads in rank order, and n_unique /
+ * bigcounts are exact for that order (tables and n_occupied do not depend on
+ * the order). */
+enum { KH_GROUP_BROADCAST = 0, KH_GROUP_EXCHANGE = 1 };
+int kh_group_create_mode(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables, int world, int rank,
+                         int nlocal, const int *devices, const unsigned char *uid, int mode, kh_group **out);
+int kh_group_create_hosted_mode(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables, int world,
+                                int rank, int device, const kh_transport *transport, int mode, kh_group **out);
+int kh_group_mode(kh_group *grp, int *mode);
+/* bins [lo, lo + size) of table `table` held by rank `rank` (any rank) */
+int kh_group_rank_slice(kh_group *grp, int rank, int table, uint64_t *lo, uint64_t *size);
 int kh_group_counters(kh_group *grp, uint64_t *n_unique, uint64_t *n_occupied);   /* collective */
 
 #ifdef __cplusplus

@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("KHMER_AMD_LIB") or os.path.join(_HERE, "libkhmer_hip.
 KH_OK, KH_EVALUE, KH_EFILE, KH_EATTR, KH_ENOMEM, KH_EDEVICE, KH_ERUNTIME, KH_END = range(8)
 STORAGE_BYTE, STORAGE_BIT, STORAGE_NIBBLE = 1, 2, 7
 HASH_TWOBIT, HASH_MURMUR = 0, 1
+GROUP_BROADCAST, GROUP_EXCHANGE = 0, 1   # include/khmer_hip.h KH_GROUP_*
 
 if not os.path.exists(LIB_PATH):
     raise ImportError("khmer_amd: %s is not built; run `make -C khmer_amd/csrc` "
@@ -66,6 +67,11 @@ SIGNATURES = {
     "kh_group_slice": (i32, [P, i32, i32, PU64, PU64]),
     "kh_group_consume_packed_fixed_device": (i32, [P, ctypes.POINTER(P), u64, u64]),
     "kh_group_counters": (i32, [P, PU64, PU64]),
+    "kh_group_create_mode": (i32, [i32, i32, i32, PU64, i32, i32, i32, i32, PI, ctypes.c_char_p, i32,
+                                   ctypes.POINTER(P)]),
+    "kh_group_create_hosted_mode": (i32, [i32, i32, i32, PU64, i32, i32, i32, i32, P, i32, ctypes.POINTER(P)]),
+    "kh_group_mode": (i32, [P, PI]),
+    "kh_group_rank_slice": (i32, [P, i32, i32, PU64, PU64]),
     "kh_consume_parser": (i32, [P, P, i32, PU32, PU64]),
     "kh_consume_parser_filtered": (i32, [P, P, u32, u32, P, u32, i32, PU32, PU64]),
     "kh_consume_seqs": (i32, [P, ctypes.c_char_p, PU64, u64, i32, PU64]),

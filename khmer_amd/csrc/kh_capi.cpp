@@ -1364,14 +1364,38 @@ extern "C" int kh_group_unique_id(unsigned char *out, size_t cap) {
     });
 }
 
-extern "C" int kh_group_create(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables, int world,
-                               int rank, int nlocal, const int *devices, const unsigned char *uid, kh_group **out) {
+extern "C" int kh_group_create_mode(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables,
+                                    int world, int rank, int nlocal, const int *devices, const unsigned char *uid,
+                                    int mode, kh_group **out) {
     return guard([&] {
         CHECK_PTR(sizes);
         CHECK_PTR(devices);
         CHECK_PTR(out);
         *out = nullptr;
-        ShardGroup *G = group_create(storage, hash_kind, k, sizes, n_tables, world, rank, nlocal, devices, uid);
+        if (mode != KH_GROUP_BROADCAST && mode != KH_GROUP_EXCHANGE) fail(KH_EVALUE, "unknown group mode");
+        ShardGroup *G = group_create(storage, hash_kind, k, sizes, n_tables, world, rank, nlocal, devices, uid,
+                                     mode == KH_GROUP_EXCHANGE);
+        *out = new kh_group{G};
+    });
+}
+
+extern "C" int kh_group_create(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables, int world,
+                               int rank, int nlocal, const int *devices, const unsigned char *uid, kh_group **out) {
+    return kh_group_create_mode(storage, hash_kind, k, sizes, n_tables, world, rank, nlocal, devices, uid,
+                                KH_GROUP_BROADCAST, out);
+}
+
+extern "C" int kh_group_create_hosted_mode(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables,
+                                           int world, int rank, int device, const kh_transport *transport, int mode,
+                                           kh_group **out) {
+    return guard([&] {
+        CHECK_PTR(sizes);
+        CHECK_PTR(transport);
+        CHECK_PTR(out);
+        *out = nullptr;
+        if (mode != KH_GROUP_BROADCAST && mode != KH_GROUP_EXCHANGE) fail(KH_EVALUE, "unknown group mode");
+        ShardGroup *G = group_create_hosted(storage, hash_kind, k, sizes, n_tables, world, rank, device, transport,
+                                            mode == KH_GROUP_EXCHANGE);
         *out = new kh_group{G};
     });
 }
@@ -1379,14 +1403,8 @@ extern "C" int kh_group_create(int storage, int hash_kind, int k, const uint64_t
 extern "C" int kh_group_create_hosted(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables,
                                       int world, int rank, int device, const kh_transport *transport,
                                       kh_group **out) {
-    return guard([&] {
-        CHECK_PTR(sizes);
-        CHECK_PTR(transport);
-        CHECK_PTR(out);
-        *out = nullptr;
-        ShardGroup *G = group_create_hosted(storage, hash_kind, k, sizes, n_tables, world, rank, device, transport);
-        *out = new kh_group{G};
-    });
+    return kh_group_create_hosted_mode(storage, hash_kind, k, sizes, n_tables, world, rank, device, transport,
+                                       KH_GROUP_BROADCAST, out);
 }
 
 extern "C" int kh_group_comm_info(kh_group *grp, int *nranks, int *device) {
@@ -1428,6 +1446,23 @@ extern "C" int kh_group_slice(kh_group *grp, int l, int table, uint64_t *lo, uin
         if (table < 0 || table >= g->n) fail(KH_EVALUE, "no such table");
         *lo = g->lo[(size_t)table];
         *size = g->lsz[(size_t)table];
+    });
+}
+
+extern "C" int kh_group_rank_slice(kh_group *grp, int rank, int table, uint64_t *lo, uint64_t *size) {
+    return guard([&] {
+        CHECK_PTR(grp);
+        CHECK_PTR(lo);
+        CHECK_PTR(size);
+        group_rank_slice(grp->G, rank, table, lo, size);
+    });
+}
+
+extern "C" int kh_group_mode(kh_group *grp, int *mode) {
+    return guard([&] {
+        CHECK_PTR(grp);
+        CHECK_PTR(mode);
+        *mode = group_exchange(grp->G) ? KH_GROUP_EXCHANGE : KH_GROUP_BROADCAST;
     });
 }
 

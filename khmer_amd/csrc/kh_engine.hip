@@ -161,7 +161,7 @@ static void bcmap_merge(Graph *g, uint64_t nkeys, uint64_t n_ff) {
 // record buffers for a pass holding `recs` records (level-1 out / level-2 out;
 // the dead level-1 buffer later holds the winner lists).  Sized from the
 // device's exact count, so a shard only holds the records it owns.
-static void ensure_recs(Graph *g, uint64_t recs) {
+static void ensure_recs(Graph *g, uint64_t recs, bool level2 = true) {
     Workspace &w = g->ws;
     if (recs <= w.cap_recs && w.rec1) return;
     // grow by half (fewer reallocations) while that fits next to everything
@@ -169,7 +169,8 @@ static void ensure_recs(Graph *g, uint64_t recs) {
     uint64_t grow = w.cap_recs + w.cap_recs / 2;
     size_t freeb = 0, total = 0;
     if (hipMemGetInfo(&freeb, &total) == hipSuccess) {
-        const double fit = ((double)freeb + 16.0 * (double)w.cap_recs) * 0.95 / 16.0 - 64.0;
+        const double per = level2 ? 16.0 : 8.0;   // bytes per record of capacity (one or two buffers)
+        const double fit = ((double)freeb + per * (double)w.cap_recs) * 0.95 / per - 64.0;
         grow = std::min<uint64_t>(grow, fit > 0 ? (uint64_t)fit : 0);
     } else {
         (void)hipGetLastError();
@@ -179,6 +180,7 @@ static void ensure_recs(Graph *g, uint64_t recs) {
     for (uint64_t **pp : {&w.rec1, &w.rec2}) {
         if (*pp) KH_HIP(hipFree(*pp));
         *pp = nullptr;
+        if (!level2 && pp == &w.rec2) continue;   // level-1 only (an exchange-mode view)
         // KH_REC_MALLOC_FLAGS: development knob, hipExtMallocWithFlags flags for
         // the record buffers (placement experiments); plain hipMalloc otherwise
         static const char *fl = getenv("KH_REC_MALLOC_FLAGS");
@@ -334,7 +336,7 @@ static OwnL1FFn<Src> own_l1f_kernel(int kpt, bool tw) {
 }
 template <class Src>
 using L1FFn = void (*)(Params, Src, uint64_t, uint64_t, int, int, const uint64_t *, unsigned long long *, uint64_t *,
-                       uint64_t *, int);
+                       uint64_t *, int, uint32_t);
 // fixed-length 2-bit reads whose tiles span at most L1F_TW packed words take
 // the LDS-staged variant (k_scatter_l1f<..., TW = true>)
 template <class Src>
@@ -524,6 +526,18 @@ void engine_collect_events(Graph *g) {
     g->ev_next = 0;
 }
 #define TIMED(name, ...) do { KTimer kt_(g, name); __VA_ARGS__; } while (0)
+#define TIMED_G(gr, name, ...) do { KTimer kt_(gr, name); __VA_ARGS__; } while (0)
+// an exchange-mode view's kernel timings go to its shard's statistics
+static void move_kstats(Graph *dst, Graph *src) {
+    engine_collect_events(src);
+    for (auto &p : src->kstats) {
+        auto it = std::find_if(dst->kstats.begin(), dst->kstats.end(), [&](auto &x) { return x.first == p.first; });
+        if (it == dst->kstats.end()) { dst->kstats.push_back({p.first, Graph::KStat{}}); it = dst->kstats.end() - 1; }
+        it->second.ms += p.second.ms;
+        it->second.n += p.second.n;
+    }
+    src->kstats.clear();
+}
 
 // level-1 scatter instance for a tail mode and k-mers per thread (8 / nt)
 template <class Src>
@@ -740,6 +754,91 @@ static void winners_fine(Graph *g, PassState &ps) {
     KH_HIP(hipGetLastError());
 }
 
+// apply, crossing bins and the winner partition of a pass whose level-2
+// records are in place (fixed-capacity regions when l2f, else the exact
+// offsets off2)
+static void pass_apply(Graph *g, PassState &ps, bool l2f) {
+    const Params &P = g->prm;
+    Workspace &w = g->ws;
+    hipStream_t st = g->stream;
+    const PassGeo &q = ps.q;
+    const uint64_t nkmers = ps.nkmers;
+    const bool bigc = ps.bigc;
+    // apply (winner segments -> first half of the dead level-1 buffer)
+    uint32_t *win = (uint32_t *)w.rec1;
+    uint32_t *wout = win + w.cap_recs;
+    ps.win = win;
+    ps.wout = wout;
+    ApplyArgs &A = ps.A;
+    A.rlo = l2f ? w.reg_base : w.off2;
+    A.rhi = l2f ? w.reg_cur : w.off2 + 1;
+    A.rec = w.rec2;
+    A.tab = g->d_tab;
+    A.win = win;
+    A.wcnt = w.wcnt;
+    A.fullf = w.fullf;
+    A.xent = wout;       // free until scatter_w: crossing entries live there meanwhile
+    A.xseg = w.xseg;
+    A.ctr = w.ctr;
+    A.rprefix[0] = 0;
+    for (int i = 0; i < P.n; i++)
+        A.rprefix[i + 1] = A.rprefix[i] + ((P.lsz[i] + (1ull << P.s0) - 1) >> P.s0);
+    // coarse windows of 2^cjs k-mers (<= 64), each a fine window multiple;
+    // window c may hold (its k-mers) x (tables) winners, the capacity of its
+    // range of the winner array (the dead level-1 records)
+    ps.coarse = coarse_winners(g);
+    A.coarse = ps.coarse ? 1 : 0;
+    A.cjs = std::max(q.js, ceil_log2(nkmers) - 6);
+    A.wco = win;
+    A.cw_cur = nullptr;
+    if (ps.coarse) {
+        ps.ncw = (uint32_t)((nkmers + (1ull << A.cjs) - 1) >> A.cjs);
+        ps.fpc = 1u << (A.cjs - q.js);
+        if (!w.cw_cur) {
+            KH_HIP(hipMalloc((void **)&w.cw_cur, MAX_CW * 8));
+            KH_HIP(hipMalloc((void **)&w.cmbase, (MAX_CW + 1) * 8));
+            KH_HIP(hipMalloc((void **)&w.cnk, MAX_CW * 4));
+        }
+        std::vector<unsigned long long> cb(MAX_CW, 0);
+        uint64_t acc = 0;
+        for (uint32_t c = 0; c < ps.ncw; c++) {
+            cb[c] = acc;
+            acc += std::min<uint64_t>(1ull << A.cjs, nkmers - ((uint64_t)c << A.cjs)) * (uint64_t)P.n;
+        }
+        if (acc > w.cap_recs) fail(KH_EDEVICE, "winner capacity exceeds the record buffer");
+        KH_HIP(hipMemcpyAsync(w.cw_cur, cb.data(), MAX_CW * 8, hipMemcpyHostToDevice, st));
+        A.cw_cur = w.cw_cur;
+    }
+    const unsigned agrid = (unsigned)std::min<uint64_t>(q.regions, 256 * 2);
+    if (P.kind == BIT && ps.coarse)   // one 1024-thread workgroup per CU (the staging array), else two of 512
+        TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit<1024>, dim3((unsigned)std::min<uint64_t>(q.regions, device_cus(g))),
+                                              dim3(1024), lds_apply(P, true), st, P, A));
+    else if (P.kind == BIT)
+        TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit<APPLY_THREADS>, dim3(agrid), dim3(APPLY_THREADS),
+                                              lds_apply(P), st, P, A));
+    else if (P.kind == NIBBLE)
+        TIMED("apply_nibble", hipLaunchKernelGGL(apply_count_kernel<NIBBLE>(P), dim3(agrid_count(g, q)),
+                                                 dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
+    else
+        TIMED("apply_byte", hipLaunchKernelGGL(apply_count_kernel<BYTE>(P), dim3(agrid_count(g, q)),
+                                               dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
+    if (bigc)
+        TIMED("crossing", hipLaunchKernelGGL(k_crossing, dim3(1024), dim3(256), 0, st, P, w.rec2, w.xseg, wout,
+                                             w.ctr, w.fullf));
+
+    if (ps.coarse) {
+        winners_fine(g, ps);
+        return;
+    }
+    // winners -> k-mer windows
+    const size_t wmeta = W_RPC * 8 + (W_RPC + 4) * 4;
+    TIMED("hist_w", hipLaunchKernelGGL(k_hist_w, dim3(q.nchw), dim3(PT_THREADS), wmeta + (size_t)q.FJ * 4, st, P, A,
+                                       q.js, q.FJ, q.nchw, w.mcnt));
+    TIMED("scan", scan_counts(g, w.mcnt, w.moff, (uint64_t)q.FJ * q.nchw));
+    TIMED("scatter_w", hipLaunchKernelGGL(w_kernel(), dim3(q.nchw), dim3(PT_THREADS),
+                                          lds_scatter_w(q.FJ), st, P, A, q.js, q.FJ, q.nchw, w.moff, wout));
+}
+
 template <class Src>
 static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     if (nkmers > MAX_PASS_KMERS) fail(KH_EVALUE, "device batch too large (more than 3200 * 2^20 k-mers)");
@@ -814,7 +913,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                                                        dim3(nwg), dim3(L1_THREADS),
                                                        lds_scatter_l1f(P, window, (int)tk), st, P, src, nkmers, kpw,
                                                        t0, nt, w.bkt_base, (unsigned long long *)w.bkt_cur, w.rec1,
-                                                       w.ctr, l1f_blk_sh()));
+                                                       w.ctr, l1f_blk_sh(), 0u));
             }
         } else if (use_own_filter(g)) {
             nrec = own_filter(g, src, nkmers, window);
@@ -906,80 +1005,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
         }
         break;
     }
-    const bool l2f = fast;
-    // apply (winner segments -> first half of the dead level-1 buffer)
-    uint32_t *win = (uint32_t *)w.rec1;
-    uint32_t *wout = win + w.cap_recs;
-    ps.win = win;
-    ps.wout = wout;
-    ApplyArgs &A = ps.A;
-    A.rlo = l2f ? w.reg_base : w.off2;
-    A.rhi = l2f ? w.reg_cur : w.off2 + 1;
-    A.rec = w.rec2;
-    A.tab = g->d_tab;
-    A.win = win;
-    A.wcnt = w.wcnt;
-    A.fullf = w.fullf;
-    A.xent = wout;       // free until scatter_w: crossing entries live there meanwhile
-    A.xseg = w.xseg;
-    A.ctr = w.ctr;
-    A.rprefix[0] = 0;
-    for (int i = 0; i < P.n; i++)
-        A.rprefix[i + 1] = A.rprefix[i] + ((P.lsz[i] + (1ull << P.s0) - 1) >> P.s0);
-    // coarse windows of 2^cjs k-mers (<= 64), each a fine window multiple;
-    // window c may hold (its k-mers) x (tables) winners, the capacity of its
-    // range of the winner array (the dead level-1 records)
-    ps.coarse = coarse_winners(g);
-    A.coarse = ps.coarse ? 1 : 0;
-    A.cjs = std::max(q.js, ceil_log2(nkmers) - 6);
-    A.wco = win;
-    A.cw_cur = nullptr;
-    if (ps.coarse) {
-        ps.ncw = (uint32_t)((nkmers + (1ull << A.cjs) - 1) >> A.cjs);
-        ps.fpc = 1u << (A.cjs - q.js);
-        if (!w.cw_cur) {
-            KH_HIP(hipMalloc((void **)&w.cw_cur, MAX_CW * 8));
-            KH_HIP(hipMalloc((void **)&w.cmbase, (MAX_CW + 1) * 8));
-            KH_HIP(hipMalloc((void **)&w.cnk, MAX_CW * 4));
-        }
-        std::vector<unsigned long long> cb(MAX_CW, 0);
-        uint64_t acc = 0;
-        for (uint32_t c = 0; c < ps.ncw; c++) {
-            cb[c] = acc;
-            acc += std::min<uint64_t>(1ull << A.cjs, nkmers - ((uint64_t)c << A.cjs)) * (uint64_t)P.n;
-        }
-        if (acc > w.cap_recs) fail(KH_EDEVICE, "winner capacity exceeds the record buffer");
-        KH_HIP(hipMemcpyAsync(w.cw_cur, cb.data(), MAX_CW * 8, hipMemcpyHostToDevice, st));
-        A.cw_cur = w.cw_cur;
-    }
-    const unsigned agrid = (unsigned)std::min<uint64_t>(q.regions, 256 * 2);
-    if (P.kind == BIT && ps.coarse)   // one 1024-thread workgroup per CU (the staging array), else two of 512
-        TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit<1024>, dim3((unsigned)std::min<uint64_t>(q.regions, device_cus(g))),
-                                              dim3(1024), lds_apply(P, true), st, P, A));
-    else if (P.kind == BIT)
-        TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit<APPLY_THREADS>, dim3(agrid), dim3(APPLY_THREADS),
-                                              lds_apply(P), st, P, A));
-    else if (P.kind == NIBBLE)
-        TIMED("apply_nibble", hipLaunchKernelGGL(apply_count_kernel<NIBBLE>(P), dim3(agrid_count(g, q)),
-                                                 dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
-    else
-        TIMED("apply_byte", hipLaunchKernelGGL(apply_count_kernel<BYTE>(P), dim3(agrid_count(g, q)),
-                                               dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
-    if (bigc)
-        TIMED("crossing", hipLaunchKernelGGL(k_crossing, dim3(1024), dim3(256), 0, st, P, w.rec2, w.xseg, wout,
-                                             w.ctr, w.fullf));
-
-    if (ps.coarse) {
-        winners_fine(g, ps);
-        return ps;
-    }
-    // winners -> k-mer windows
-    const size_t wmeta = W_RPC * 8 + (W_RPC + 4) * 4;
-    TIMED("hist_w", hipLaunchKernelGGL(k_hist_w, dim3(q.nchw), dim3(PT_THREADS), wmeta + (size_t)q.FJ * 4, st, P, A,
-                                       q.js, q.FJ, q.nchw, w.mcnt));
-    TIMED("scan", scan_counts(g, w.mcnt, w.moff, (uint64_t)q.FJ * q.nchw));
-    TIMED("scatter_w", hipLaunchKernelGGL(w_kernel(), dim3(q.nchw), dim3(PT_THREADS),
-                                          lds_scatter_w(q.FJ), st, P, A, q.js, q.FJ, q.nchw, w.moff, wout));
+    pass_apply(g, ps, fast);
     return ps;
 }
 
@@ -1550,6 +1576,7 @@ void graph_prepare_params(Graph *g) {
     P.s2 = std::min({10, ceil_log2(maxreg), std::max(half + 1, 1)});
     static const int s2_env = env_seg("KH_S2", 0);   // development: force the level-2 fan-out
     if (s2_env > 0) P.s2 = std::min({10, s2_env, std::max(ceil_log2(maxreg), 1)});
+    if (g->force_s2 >= 0) P.s2 = g->force_s2;
     const uint64_t span = 1ull << (P.s0 + P.s2);
     uint64_t base = 0, byteoff = 0;
     for (int i = 0; i < g->n; i++) {
@@ -1626,7 +1653,17 @@ static void set_lds_limits() {
     (void)hipGetLastError();
 }
 
+// A graph holding bins [lo_i, hi_i) of every table: the contiguous 8-bin
+// aligned slice of shard `rank` of `world` (shard_lo), or explicit bounds
+// (blo/bhi, exchange-mode groups).  tables = false builds the geometry and
+// workspace only (an exchange-mode rank's unsharded level-1 view).
+static Graph *graph_build(int kind, int hash, int k, const uint64_t *sizes, int n, int device, int world, int rank,
+                          const uint64_t *blo, const uint64_t *bhi, int force_s2, bool tables);
 Graph *graph_create_shard(int kind, int hash, int k, const uint64_t *sizes, int n, int device, int world, int rank) {
+    return graph_build(kind, hash, k, sizes, n, device, world, rank, nullptr, nullptr, -1, true);
+}
+static Graph *graph_build(int kind, int hash, int k, const uint64_t *sizes, int n, int device, int world, int rank,
+                          const uint64_t *blo, const uint64_t *bhi, int force_s2, bool tables) {
     if (n < 1 || n > MAXT) fail(KH_EVALUE, "number of tables must be in [1, 32]");
     if (kind != BYTE && kind != BIT && kind != NIBBLE) fail(KH_EVALUE, "unknown storage kind");
     if (hash == TWOBIT && (k < 1 || k > 32)) fail(KH_EVALUE, "k-mer size must be <= 32 for 2-bit hashing");
@@ -1647,7 +1684,8 @@ Graph *graph_create_shard(int kind, int hash, int k, const uint64_t *sizes, int 
         if (sizes[i] == 0) fail(KH_EVALUE, "table size must be > 0");
         g->sizes.push_back(sizes[i]);
         // contiguous slices, 8-bin aligned so Bit/Nibble slices start on a byte
-        const uint64_t lo = shard_lo(sizes[i], world, rank), hi = shard_lo(sizes[i], world, rank + 1);
+        const uint64_t lo = blo ? blo[i] : shard_lo(sizes[i], world, rank);
+        const uint64_t hi = bhi ? bhi[i] : shard_lo(sizes[i], world, rank + 1);
         g->lo.push_back(lo);
         g->lsz.push_back(hi - lo);
         // storage.hh:127-140 (bit), 297-310 (nibble), 502-511 (byte); a slice
@@ -1655,9 +1693,14 @@ Graph *graph_create_shard(int kind, int hash, int k, const uint64_t *sizes, int 
         const uint64_t m = hi - lo;
         g->nbytes.push_back(kind == BIT ? m / 8 + 1 : kind == NIBBLE ? m / 2 + 1 : m);
     }
+    g->force_s2 = force_s2;
     KH_HIP(hipSetDevice(device));
     set_lds_limits();
     graph_prepare_params(g.get());
+    if (!tables) {
+        KH_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+        return g.release();
+    }
     uint64_t arena = 0;
     for (int i = 0; i < n; i++) arena = g->prm.tbyte[i] + (g->nbytes[(size_t)i] + 255) / 256 * 256;
     g->arena_bytes = arena;
@@ -1727,6 +1770,14 @@ namespace kh {
 struct ShardGroup {
     int world = 1, rank0 = 0, nlocal = 1;
     std::vector<Graph *> shards;
+    // exchange mode (Option A): each rank hashes only its own reads into the
+    // unsharded level-1 buckets (views[l]: geometry + workspace, no tables)
+    // and sends every bucket to its owner; rank r owns buckets [B[r], B[r+1])
+    // = bins [blo, bhi) of each table ([world][n])
+    bool a2a = false;
+    std::vector<Graph *> views;
+    std::vector<uint32_t> B;
+    std::vector<uint64_t> blo, bhi;
     ncclComm_t comm = nullptr;
     ncclComm_t comm_b = nullptr;     // source-read broadcasts (own stream, overlapped with compute)
     bool hosted = false;             // one shard per process, collectives through host callbacks
@@ -1749,6 +1800,8 @@ struct ShardGroup {
         // source reads in flight: two slots filled on the transfer stream
         // (RCCL broadcast on comm_b; a device copy in loopback) while the
         // compute stream consumes the other one
+        uint64_t *seg = nullptr;
+        uint64_t cap_seg = 0;        // exchange mode: level-2 segment starts and ends
         uint64_t *slot[2] = {nullptr, nullptr};
         uint64_t cap_slot[2] = {0, 0};
         hipStream_t st_x = nullptr;
@@ -1764,7 +1817,7 @@ struct ShardGroup {
             auto &lc = loc[l];
             if (lc.st_x) (void)hipStreamSynchronize(lc.st_x);
             for (void *p : {(void *)lc.src, (void *)lc.recv, (void *)lc.ws, (void *)lc.ws_all, (void *)lc.roff,
-                            (void *)lc.flist, (void *)lc.fall, (void *)lc.slot[0], (void *)lc.slot[1]})
+                            (void *)lc.flist, (void *)lc.fall, (void *)lc.slot[0], (void *)lc.slot[1], (void *)lc.seg})
                 if (p) (void)hipFree(p);
             for (int b = 0; b < 2; b++) {
                 if (lc.ev_ready[b]) (void)hipEventDestroy(lc.ev_ready[b]);
@@ -1776,6 +1829,7 @@ struct ShardGroup {
         if (comm_b) (void)ncclCommDestroy(comm_b);
         if (comm) (void)ncclCommDestroy(comm);
         for (Graph *g : shards) delete g;
+        for (Graph *g : views) delete g;
     }
 };
 
@@ -1833,8 +1887,54 @@ void group_unique_id(unsigned char *out, size_t n) {
     memcpy(out, &id, sizeof id);
 }
 
+// Exchange-mode ownership: the unsharded geometry's level-1 buckets (2^(s0+s2)
+// bins each, tables back to back at V.tbase) in `world` contiguous ranges;
+// rank r owns buckets [B[r], B[r+1]), i.e. bins [blo, bhi) of every table.
+// Its shard's own geometry (same s2) then numbers those buckets 0, 1, ... in
+// the same order with the same in-bucket offsets, so level-1 records travel
+// unchanged.
+static void a2a_plan(const Params &V, const uint64_t *sizes, int n, int world, std::vector<uint32_t> &B,
+                     std::vector<uint64_t> &blo, std::vector<uint64_t> &bhi) {
+    const uint64_t span = 1ull << (V.s0 + V.s2);
+    B.assign(world + 1, 0);
+    for (int r = 0; r <= world; r++) B[r] = (uint32_t)((uint64_t)V.F1 * (uint64_t)r / (uint64_t)world);
+    blo.assign((size_t)world * n, 0);
+    bhi.assign((size_t)world * n, 0);
+    for (int r = 0; r < world; r++)
+        for (int i = 0; i < n; i++) {
+            auto bin_of = [&](uint64_t bkt) -> uint64_t {
+                const uint64_t x = bkt * span;
+                return x <= V.tbase[i] ? 0 : std::min<uint64_t>(sizes[i], x - V.tbase[i]);
+            };
+            blo[(size_t)r * n + i] = bin_of(B[r]);
+            bhi[(size_t)r * n + i] = bin_of(B[r + 1]);
+        }
+}
+
+static void group_make_shards(ShardGroup *G, int kind, int hash, int k, const uint64_t *sizes, int n,
+                              const int *devices, bool exchange) {
+    const int world = G->world;
+    if (exchange) {
+        if (hash != TWOBIT) fail(KH_EVALUE, "exchange mode takes 2-bit hashed graphs");
+        for (int l = 0; l < G->nlocal; l++)
+            G->views.push_back(graph_build(kind, hash, k, sizes, n, devices[l], 1, 0, nullptr, nullptr, -1, false));
+        const Params &V = G->views[0]->prm;
+        if (V.F1 < (uint32_t)world) fail(KH_EVALUE, "exchange mode needs at least one level-1 bucket per rank");
+        if (V.F1 > 1024) fail(KH_EVALUE, "exchange mode supports at most 1024 level-1 buckets");
+        a2a_plan(V, sizes, n, world, G->B, G->blo, G->bhi);
+        G->a2a = true;
+    }
+    for (int l = 0; l < G->nlocal; l++) {
+        const int r = G->rank0 + l;
+        G->shards.push_back(exchange ? graph_build(kind, hash, k, sizes, n, devices[l], world, r, &G->blo[(size_t)r * n],
+                                                   &G->bhi[(size_t)r * n], G->views[0]->prm.s2, true)
+                                     : graph_create_shard(kind, hash, k, sizes, n, devices[l], world, r));
+        G->shards.back()->grouped = true;
+    }
+}
+
 ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank, int nlocal,
-                         const int *devices, const unsigned char *uid) {
+                         const int *devices, const unsigned char *uid, int exchange) {
     if (world < 1 || world > 64) fail(KH_EVALUE, "group size must be in [1, 64]");
     if (nlocal != 1 && nlocal != world) fail(KH_EVALUE, "a process holds one shard (RCCL) or all shards (loopback)");
     if (nlocal == 1 && (rank < 0 || rank >= world)) fail(KH_EVALUE, "invalid rank");
@@ -1842,10 +1942,7 @@ ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n
     G->world = world;
     G->nlocal = nlocal;
     G->rank0 = nlocal == world ? 0 : rank;
-    for (int l = 0; l < nlocal; l++) {
-        G->shards.push_back(graph_create_shard(kind, hash, k, sizes, n, devices[l], world, G->rank0 + l));
-        G->shards.back()->grouped = true;
-    }
+    group_make_shards(G.get(), kind, hash, k, sizes, n, devices, exchange != 0);
     G->loc.resize(nlocal);
     if (nlocal == 1 && world > 1) {
         if (!uid) fail(KH_EVALUE, "an RCCL group needs the unique id of rank 0");
@@ -1860,7 +1957,7 @@ ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n
 }
 
 ShardGroup *group_create_hosted(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank,
-                                int device, const kh_transport *t) {
+                                int device, const kh_transport *t, int exchange) {
     if (world < 1 || world > 64) fail(KH_EVALUE, "group size must be in [1, 64]");
     if (rank < 0 || rank >= world) fail(KH_EVALUE, "invalid rank");
     if (!t->allgather || !t->broadcast || !t->alltoallv) fail(KH_EVALUE, "incomplete host transport");
@@ -1870,8 +1967,7 @@ ShardGroup *group_create_hosted(int kind, int hash, int k, const uint64_t *sizes
     G->rank0 = rank;
     G->hosted = true;
     G->tp = *t;
-    G->shards.push_back(graph_create_shard(kind, hash, k, sizes, n, device, world, rank));
-    G->shards.back()->grouped = true;
+    group_make_shards(G.get(), kind, hash, k, sizes, n, &device, exchange != 0);
     G->loc.resize(1);
     KH_HIP(hipSetDevice(device));
     KH_HIP(hipMalloc((void **)&G->d_red, 256 * 8));
@@ -2054,6 +2150,404 @@ static void group_merge_full(ShardGroup *G, std::vector<PassState> &ps) {
     KH_HIP(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------
+// Exchange mode (Option A, SURVEY.md §8(e) "north star"): every rank hashes
+// only its own reads.  A pass takes the next chunk of every rank's reads; the
+// pass's stream is the rank chunks in rank order (k-mer index j = rank *
+// stride + index in the chunk), so the exact counters follow that order.
+//   1. level 1 of the own chunk into the unsharded level-1 buckets (view)
+//   2. every rank's bucket bases and fill levels (allgather)
+//   3. bucket range [B[d], B[d+1]) to its owner d (grouped ncclSend/ncclRecv;
+//      host transport: alltoallv; loopback: device copies)
+//   4. the owner's level 2 over its (source, bucket) segments, apply, winners
+//   5. winners routed by window, bigcount tallies merged (as Option B)
+//   6. finalize of the own chunk's k-mers; bigcount events replicated
+
+// level 1 of one chunk in the unsharded geometry; a bucket overflow grows the
+// capacity margin and redoes it (the chunk is still in place)
+template <class Src>
+static void a2a_level1(Graph *V, const Src &src, uint64_t nkmers, uint32_t jbase) {
+    const Params &P = V->prm;
+    Workspace &w = V->ws;
+    hipStream_t st = V->stream;
+    ws_prepare(V, pass_geo(P, nkmers));
+    const uint64_t F1 = P.F1;
+    for (;;) {
+        const uint64_t cap1 = bkt_plan(V, nkmers);
+        ensure_recs(V, cap1, false);
+        KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
+        hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)((F1 + 255) / 256)), dim3(256), 0, st, w.bkt_base,
+                           (unsigned long long *)w.bkt_cur, (uint64_t)F1);
+        const uint32_t nwg = l1f_workgroups(V, nkmers);
+        for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
+            const int nt = std::min(L1_MAX_RPT, P.n - t0);
+            const int rpt = l1f_rpt();
+            int kpt = 1;
+            while (kpt * 2 * nt <= rpt) kpt *= 2;
+            const uint64_t tk = (uint64_t)L1_THREADS * kpt;
+            const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
+            TIMED_G(V, "scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt, l1f_tw(src, kpt)), dim3(nwg),
+                                                        dim3(L1_THREADS), lds_scatter_l1f(P, false, (int)tk), st, P,
+                                                        src, nkmers, kpw, t0, nt, w.bkt_base,
+                                                        (unsigned long long *)w.bkt_cur, w.rec1, w.ctr, l1f_blk_sh(),
+                                                        jbase));
+        }
+        uint64_t err = 0;
+        KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
+        KH_HIP(hipStreamSynchronize(st));
+        if (!(err & 8)) break;
+        if (V->cap_sigma < 72.0) {
+            V->cap_sigma *= 3.0;
+            continue;
+        }
+        fail(KH_EDEVICE, "exchange mode: a level-1 bucket overflowed at the largest capacity margin (skewed input)");
+    }
+    KH_HIP(hipGetLastError());
+}
+
+// every source's bucket bases and fill levels: meta[s][0..F1] = bases,
+// meta[s][F1+1 .. 2F1+1] = ends (the last entry repeats the final base)
+static void a2a_meta(ShardGroup *G, std::vector<uint64_t> &meta) {
+    const int W = G->world, NL = G->nlocal;
+    const uint64_t F1 = G->views[0]->prm.F1, M = 2 * (F1 + 1);
+    meta.assign((size_t)W * M, 0);
+    for (int l = 0; l < NL; l++) {
+        Graph *V = G->views[l];
+        KH_HIP(hipSetDevice(V->device));
+        uint64_t *h = meta.data() + (size_t)(G->rank0 + l) * M;
+        KH_HIP(hipMemcpyAsync(h, V->ws.bkt_base, (F1 + 1) * 8, hipMemcpyDeviceToHost, V->stream));
+        KH_HIP(hipMemcpyAsync(h + F1 + 1, V->ws.bkt_cur, F1 * 8, hipMemcpyDeviceToHost, V->stream));
+        KH_HIP(hipStreamSynchronize(V->stream));
+        h[2 * F1 + 1] = h[F1];
+    }
+    if (per_rank(G)) {
+        Graph *V = G->views[0];
+        auto &lc = G->loc[0];
+        ensure((void **)&lc.seg, &lc.cap_seg, (uint64_t)W * M, 8);
+        uint64_t *d_mine = lc.seg + (size_t)G->rank0 * M;
+        KH_HIP(hipMemcpyAsync(d_mine, meta.data() + (size_t)G->rank0 * M, M * 8, hipMemcpyHostToDevice, V->stream));
+        std::vector<uint64_t> tmp(M);
+        // allgather into a separate device block, then back to the host
+        uint64_t *d_all = nullptr;
+        KH_HIP(hipMalloc((void **)&d_all, (size_t)W * M * 8));
+        coll_allgather_u64(G, V->stream, d_mine, d_all, M);
+        KH_HIP(hipMemcpyAsync(meta.data(), d_all, (size_t)W * M * 8, hipMemcpyDeviceToHost, V->stream));
+        KH_HIP(hipStreamSynchronize(V->stream));
+        KH_HIP(hipFree(d_all));
+    }
+}
+
+// the records of rank `s`'s buckets [B[r], B[r+1]) land at rbase[s] of
+// owner r's level-1 buffer
+static void a2a_exchange(ShardGroup *G, const std::vector<uint64_t> &meta, std::vector<std::vector<uint64_t>> &rbase) {
+    const int W = G->world, NL = G->nlocal;
+    const uint64_t F1 = G->views[0]->prm.F1, M = 2 * (F1 + 1);
+    auto base = [&](int s, uint32_t b) { return meta[(size_t)s * M + b]; };
+    rbase.assign(NL, std::vector<uint64_t>(W + 1, 0));
+    for (int l = 0; l < NL; l++) {
+        const int r = G->rank0 + l;
+        uint64_t acc = 0;
+        for (int s = 0; s < W; s++) {
+            rbase[l][s] = acc;
+            acc += base(s, G->B[r + 1]) - base(s, G->B[r]);
+        }
+        rbase[l][W] = acc;
+    }
+    if (G->comm) {
+        Graph *g = G->shards[0];
+        Graph *V = G->views[0];
+        const int r = G->rank0;
+        KH_HIP(hipSetDevice(g->device));
+        KH_HIP(hipStreamSynchronize(V->stream));
+        const uint64_t own = base(r, G->B[r + 1]) - base(r, G->B[r]);
+        if (own)
+            KH_HIP(hipMemcpyAsync(g->ws.rec1 + rbase[0][r], V->ws.rec1 + base(r, G->B[r]), own * 8,
+                                  hipMemcpyDeviceToDevice, g->stream));
+        KH_NCCL(ncclGroupStart());
+        for (int d = 0; d < W; d++) {
+            if (d == r) continue;
+            const uint64_t c = base(r, G->B[d + 1]) - base(r, G->B[d]);
+            if (c) KH_NCCL(ncclSend(V->ws.rec1 + base(r, G->B[d]), c, ncclUint64, d, G->comm, g->stream));
+            const uint64_t cin = base(d, G->B[r + 1]) - base(d, G->B[r]);
+            if (cin) KH_NCCL(ncclRecv(g->ws.rec1 + rbase[0][d], cin, ncclUint64, d, G->comm, g->stream));
+        }
+        KH_NCCL(ncclGroupEnd());
+    } else if (G->hosted) {
+        Graph *g = G->shards[0];
+        Graph *V = G->views[0];
+        const int r = G->rank0;
+        KH_HIP(hipSetDevice(g->device));
+        std::vector<uint64_t> sb(W), rb(W);
+        for (int d = 0; d < W; d++) {
+            sb[d] = 8 * (base(r, G->B[d + 1]) - base(r, G->B[d]));
+            rb[d] = 8 * (rbase[0][d + 1] - rbase[0][d]);
+        }
+        const uint64_t n0 = base(r, G->B[0]), nsend = base(r, G->B[W]) - n0;
+        std::vector<uint64_t> hs(nsend + 1), hr(rbase[0][W] + 1);
+        KH_HIP(hipMemcpyAsync(hs.data(), V->ws.rec1 + n0, nsend * 8, hipMemcpyDeviceToHost, V->stream));
+        KH_HIP(hipStreamSynchronize(V->stream));
+        host_rc(G->tp.alltoallv(G->tp.ctx, hs.data(), sb.data(), hr.data(), rb.data()), "alltoallv");
+        KH_HIP(hipMemcpyAsync(g->ws.rec1, hr.data(), rbase[0][W] * 8, hipMemcpyHostToDevice, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+    } else {
+        for (int l = 0; l < NL; l++) KH_HIP(hipStreamSynchronize(G->views[l]->stream));
+        for (int l = 0; l < NL; l++) {
+            const int r = G->rank0 + l;
+            Graph *g = G->shards[l];
+            KH_HIP(hipSetDevice(g->device));
+            for (int s = 0; s < W; s++) {
+                const uint64_t c = rbase[l][s + 1] - rbase[l][s];
+                if (c)
+                    KH_HIP(hipMemcpyAsync(g->ws.rec1 + rbase[l][s], G->views[s]->ws.rec1 + base(s, G->B[r]), c * 8,
+                                          hipMemcpyDeviceToDevice, g->stream));
+            }
+        }
+    }
+}
+
+// the owner's level 2 over its (source, bucket) segments, apply and winners
+static PassState a2a_owner_pass(ShardGroup *G, int l, const std::vector<uint64_t> &meta,
+                                const std::vector<uint64_t> &rb, uint64_t nk) {
+    const int W = G->world, r = G->rank0 + l;
+    Graph *g = G->shards[l];
+    const Params &P = g->prm;
+    Workspace &w = g->ws;
+    hipStream_t st = g->stream;
+    KH_HIP(hipSetDevice(g->device));
+    const uint64_t F1v = G->views[0]->prm.F1, M = 2 * (F1v + 1);
+    const uint32_t NB = G->B[r + 1] - G->B[r];
+    if (NB != P.F1) fail(KH_EDEVICE, "exchange mode: owner geometry does not match its bucket range");
+    PassState ps;
+    ps.q = pass_geo(P, nk);
+    ps.nkmers = nk;
+    ps.bigc = P.kind == BYTE && P.use_bigcount;
+    ws_prepare(g, ps.q);
+    KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
+    if (ps.bigc) {
+        KH_HIP(hipMemsetAsync(w.fullf, 0, (nk + 15) & ~15ull, st));
+        bcmap_clear(w, st);
+    }
+    // segment s * NB + b: source s's bucket B[r] + b inside its block of rec1
+    const uint64_t nseg = (uint64_t)W * NB;
+    std::vector<uint64_t> seg(2 * (nseg + 1));
+    for (int s = 0; s < W; s++)
+        for (uint32_t b = 0; b < NB; b++) {
+            const uint64_t bb = meta[(size_t)s * M + G->B[r] + b], b0 = meta[(size_t)s * M + G->B[r]];
+            const uint64_t e = meta[(size_t)s * M + F1v + 1 + G->B[r] + b];
+            seg[s * NB + b] = rb[s] + (bb - b0);
+            seg[nseg + 1 + s * NB + b] = rb[s] + (e - b0);
+        }
+    seg[nseg] = rb[W];
+    seg[2 * nseg + 1] = rb[W];
+    auto &lc = G->loc[l];
+    ensure((void **)&lc.seg, &lc.cap_seg, 2 * (nseg + 1), 8);
+    KH_HIP(hipMemcpyAsync(lc.seg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, st));
+    const uint64_t F2 = 1ull << P.s2, nreg = (uint64_t)P.F1 * F2;
+    // W segments per bucket: split each into parts / W so a region has as many
+    // writing workgroups (partial blocks) as reg_plan's slack allows
+    const uint32_t parts = std::max<uint32_t>(1, l2f_parts(P.F1) / (uint32_t)W);
+    for (;;) {
+        const uint64_t cap2 = reg_plan(g, nk);
+        if (cap2 > w.cap_recs) {
+            // a larger margin after an overflow: grow both buffers, keeping
+            // the received level-1 records
+            const uint64_t keep = rb[W];
+            uint64_t *tmp = nullptr;
+            KH_HIP(hipMalloc((void **)&tmp, keep * 8 + 64));
+            KH_HIP(hipMemcpyAsync(tmp, w.rec1, keep * 8, hipMemcpyDeviceToDevice, st));
+            KH_HIP(hipStreamSynchronize(st));
+            ensure_recs(g, cap2);
+            KH_HIP(hipMemcpyAsync(w.rec1, tmp, keep * 8, hipMemcpyDeviceToDevice, st));
+            KH_HIP(hipStreamSynchronize(st));
+            KH_HIP(hipFree(tmp));
+        }
+        hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)std::min<uint64_t>((nreg + 255) / 256, 4096)), dim3(256), 0, st,
+                           w.reg_base, (unsigned long long *)w.reg_cur, nreg);
+        TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(nseg * parts)),
+                                               dim3(PT_THREADS), lds_scatter_l2f(P), st, (uint32_t)NB, P.s0, P.s2,
+                                               parts, lc.seg, lc.seg + nseg + 1, w.reg_base,
+                                               (unsigned long long *)w.reg_cur, w.rec1, w.rec2, w.ctr, l2f_blk_sh()));
+        uint64_t err = 0;
+        KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
+        KH_HIP(hipStreamSynchronize(st));
+        if (!(err & 4)) break;
+        KH_HIP(hipMemsetAsync(w.ctr + CTR_ERR, 0, 8, st));
+        if (g->cap_sigma < 72.0 && recs_fit(g, nk, g->cap_sigma * 3.0)) {
+            g->cap_sigma *= 3.0;
+            continue;
+        }
+        fail(KH_EDEVICE, "exchange mode: a level-2 region overflowed at the largest capacity margin (skewed input)");
+    }
+    pass_apply(g, ps, true);
+    return ps;
+}
+
+// finalize of the own chunk (its k-mers are [r * stride, r * stride + nkc) of
+// the pass), counters, and the bigcount events of every rank merged into
+// every rank's map (ByteStorage::add's saturating sum is order-free)
+static void a2a_stage_c(ShardGroup *G, std::vector<PassState> &ps, const std::vector<SrcTwoBit> &srcs,
+                        uint64_t stride, uint64_t nkc) {
+    const int W = G->world, NL = G->nlocal;
+    std::vector<std::vector<uint64_t>> keys(W);
+    std::vector<std::vector<uint32_t>> cnts(W);
+    std::vector<uint64_t> nff(W, 0);
+    const bool bigc = ps[0].bigc;
+    for (int l = 0; l < NL; l++) {
+        const int r = G->rank0 + l;
+        Graph *g = G->shards[l];
+        Workspace &w = g->ws;
+        const Params &P = g->prm;
+        hipStream_t st = g->stream;
+        KH_HIP(hipSetDevice(g->device));
+        const uint64_t nchunk = (nkc + 15) / 16;
+        const unsigned fgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nchunk + FIN_THREADS - 1) / FIN_THREADS, 4096));
+        for (;;) {
+            if (bigc)
+                TIMED("finalize", hipLaunchKernelGGL(k_finalize<SrcTwoBit>, dim3(fgrid), dim3(FIN_THREADS), 0, st, P,
+                                                     srcs[l], nkc, w.fullf + (uint64_t)r * stride, w.ctr, w.bck, w.bcv,
+                                                     w.cap_bcmap - 1, (uint64_t *)nullptr));
+            KH_HIP(hipGetLastError());
+            KH_HIP(hipMemcpyAsync(w.h_ctr, w.ctr, CTR_N * 8, hipMemcpyDeviceToHost, st));
+            KH_HIP(hipStreamSynchronize(st));
+            if (!(bigc && (w.h_ctr[CTR_ERR] & 2))) break;
+            bcmap_alloc(w, w.cap_bcmap * 4);
+            bcmap_clear(w, st);
+            KH_HIP(hipMemsetAsync(w.ctr + CTR_NBC, 0, 16, st));    // CTR_NBC, CTR_ERR
+            KH_HIP(hipMemsetAsync(w.ctr + CTR_BCFF, 0, 8, st));
+        }
+        engine_collect_events(g);
+        if (w.h_ctr[CTR_ERR]) fail(KH_EDEVICE, "device pipeline error flag set");
+        g->n_occupied += w.h_ctr[CTR_OCC];
+        g->n_unique += w.h_ctr[CTR_UNIQUE];
+        if (!bigc) continue;
+        const uint64_t nkeys = w.h_ctr[CTR_NBC];
+        nff[r] = w.h_ctr[CTR_BCFF];
+        keys[r].resize(nkeys);
+        cnts[r].resize(nkeys);
+        if (nkeys) {
+            KH_HIP(hipMemsetAsync(w.ctr + CTR_BCOUT, 0, 8, st));
+            const unsigned grid = (unsigned)std::min<uint64_t>((w.cap_bcmap + 255) / 256, 8192);
+            hipLaunchKernelGGL(k_bc_compact, dim3(grid), dim3(256), 0, st, w.bck, w.bcv, w.cap_bcmap, w.ctr, w.bc,
+                               w.bcn);
+            KH_HIP(hipMemcpyAsync(keys[r].data(), w.bc, nkeys * 8, hipMemcpyDeviceToHost, st));
+            KH_HIP(hipMemcpyAsync(cnts[r].data(), w.bcn, nkeys * 4, hipMemcpyDeviceToHost, st));
+            KH_HIP(hipStreamSynchronize(st));
+        }
+    }
+    if (!bigc) return;
+    if (per_rank(G)) {
+        // sizes, then (key, count) pairs padded to the largest list
+        Graph *g = G->shards[0];
+        const int r = G->rank0;
+        KH_HIP(hipSetDevice(g->device));
+        uint64_t mine[2] = {keys[r].size(), nff[r]};
+        KH_HIP(hipMemcpyAsync(G->d_red + 160, mine, 16, hipMemcpyHostToDevice, g->stream));
+        coll_allgather_u64(G, g->stream, G->d_red + 160, G->d_red, 2);
+        std::vector<uint64_t> sz(2 * W);
+        KH_HIP(hipMemcpyAsync(sz.data(), G->d_red, 2 * W * 8, hipMemcpyDeviceToHost, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+        uint64_t mx = 0;
+        for (int s = 0; s < W; s++) {
+            mx = std::max<uint64_t>(mx, sz[2 * s]);
+            nff[s] = sz[2 * s + 1];
+        }
+        if (mx) {
+            std::vector<uint64_t> send(2 * mx, 0), all((size_t)W * 2 * mx);
+            for (uint64_t i = 0; i < keys[r].size(); i++) {
+                send[2 * i] = keys[r][i];
+                send[2 * i + 1] = cnts[r][i];
+            }
+            uint64_t *d = nullptr;
+            KH_HIP(hipMalloc((void **)&d, (size_t)(W + 1) * 2 * mx * 8));
+            KH_HIP(hipMemcpyAsync(d, send.data(), 2 * mx * 8, hipMemcpyHostToDevice, g->stream));
+            coll_allgather_u64(G, g->stream, d, d + 2 * mx, 2 * mx);
+            KH_HIP(hipMemcpyAsync(all.data(), d + 2 * mx, all.size() * 8, hipMemcpyDeviceToHost, g->stream));
+            KH_HIP(hipStreamSynchronize(g->stream));
+            KH_HIP(hipFree(d));
+            for (int s = 0; s < W; s++) {
+                if (s == r) continue;
+                keys[s].resize(sz[2 * s]);
+                cnts[s].resize(sz[2 * s]);
+                for (uint64_t i = 0; i < sz[2 * s]; i++) {
+                    keys[s][i] = all[(size_t)s * 2 * mx + 2 * i];
+                    cnts[s][i] = (uint32_t)all[(size_t)s * 2 * mx + 2 * i + 1];
+                }
+            }
+        }
+    }
+    for (int l = 0; l < NL; l++) {
+        Graph *g = G->shards[l];
+        auto bump = [&](uint64_t h, uint64_t f) {
+            auto it = g->bigcounts.find(h);
+            const uint64_t b = it == g->bigcounts.end() ? 255 : it->second;
+            g->bigcounts[h] = (uint16_t)std::min<uint64_t>(b + f, 65535);
+        };
+        bool any = false;
+        for (int s = 0; s < W; s++) {
+            if (nff[s]) bump(BC_EMPTY, nff[s]), any = true;
+            for (size_t i = 0; i < keys[s].size(); i++) bump(keys[s][i], cnts[s][i]), any = true;
+        }
+        if (any) g->bc_dirty = true;
+    }
+}
+
+static void group_consume_a2a(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len) {
+    const int W = G->world, NL = G->nlocal;
+    Graph *g0 = G->shards[0];
+    const uint64_t kpr = read_len - g0->k + 1;
+    // a pass: the next rpb reads of every rank; its k-mer index space W *
+    // stride (stride a multiple of 16: fullf chunks) stays below 2^32
+    const uint64_t cap = std::min<uint64_t>(g0->batch_kmers, MAX_PASS_KMERS) / (uint64_t)W;
+    const uint64_t rpb0 = std::max<uint64_t>(1, (cap > 16 ? cap - 16 : 1) / kpr);
+    const uint64_t npass = std::max<uint64_t>(1, (nreads + rpb0 - 1) / rpb0);
+    const uint64_t rpb = std::max<uint64_t>(1, (nreads + npass - 1) / npass);
+    const uint64_t stride = (rpb * kpr + 15) & ~15ull;
+    const uint64_t nk = (uint64_t)W * stride;
+    for (uint64_t r0 = 0; r0 < nreads; r0 += rpb) {
+        const uint64_t nr = std::min(rpb, nreads - r0), nkc = nr * kpr;
+        std::vector<SrcTwoBit> srcs(NL);
+        for (int l = 0; l < NL; l++) {
+            Graph *V = G->views[l];
+            KH_HIP(hipSetDevice(V->device));
+            V->use_bigcount = G->shards[l]->use_bigcount;
+            V->profile = G->shards[l]->profile;
+            SrcTwoBit sb = src_twobit(V, d_words[l]);
+            set_fixed(sb, kpr);
+            sb.koff = nullptr;
+            sb.nreads = nr;
+            sb.kbase = r0 * kpr;
+            sb.rbase = 0;
+            srcs[l] = sb;
+            a2a_level1(V, sb, nkc, (uint32_t)((uint64_t)(G->rank0 + l) * stride));
+            move_kstats(G->shards[l], V);
+        }
+        std::vector<uint64_t> meta;
+        a2a_meta(G, meta);
+        // owner buffers: the received records (level 1) and the level-2 regions
+        const uint64_t F1v = G->views[0]->prm.F1, M = 2 * (F1v + 1);
+        for (int l = 0; l < NL; l++) {
+            const int r = G->rank0 + l;
+            Graph *g = G->shards[l];
+            KH_HIP(hipSetDevice(g->device));
+            uint64_t need = 0;
+            for (int s = 0; s < W; s++) need += meta[(size_t)s * M + G->B[r + 1]] - meta[(size_t)s * M + G->B[r]];
+            ensure_recs(g, std::max(need, reg_plan(g, nk)));
+        }
+        std::vector<std::vector<uint64_t>> rb;
+        a2a_exchange(G, meta, rb);
+        std::vector<PassState> ps(NL);
+        for (int l = 0; l < NL; l++) ps[l] = a2a_owner_pass(G, l, meta, rb[l], nk);
+        group_route_winners(G, ps);
+        if (ps[0].bigc) group_merge_full(G, ps);
+        a2a_stage_c(G, ps, srcs, stride, nkc);
+    }
+    for (int l = 0; l < NL; l++) {
+        KH_HIP(hipSetDevice(G->shards[l]->device));
+        KH_HIP(hipStreamSynchronize(G->views[l]->stream));
+        KH_HIP(hipStreamSynchronize(G->shards[l]->stream));
+    }
+}
+
 // collective: every rank passes its own fixed-length packed reads (same
 // count and length on every rank); consumed as the stream rank 0, 1, ...
 void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len) {
@@ -2073,6 +2567,10 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
         KH_HIP(hipMemcpyAsync(mm, G->d_red + 142, 32, hipMemcpyDeviceToHost, g0->stream));
         KH_HIP(hipStreamSynchronize(g0->stream));
         if (mm[0] != mm[2] || mm[1] != mm[3]) fail(KH_EVALUE, "ranks passed different read counts or lengths");
+    }
+    if (G->a2a) {
+        group_consume_a2a(G, d_words, nreads, read_len);
+        return;
     }
     const uint64_t kpr = read_len - k + 1;
     const uint64_t nwords = (nreads * read_len + 31) / 32 + 1;
@@ -2210,6 +2708,19 @@ void group_counters(ShardGroup *G, uint64_t *n_unique, uint64_t *n_occupied) {
     *n_occupied = h[1];
 }
 
+void group_rank_slice(ShardGroup *G, int rank, int table, uint64_t *lo, uint64_t *size) {
+    const Graph *g = G->shards[0];
+    if (rank < 0 || rank >= G->world) fail(KH_EVALUE, "invalid rank");
+    if (table < 0 || table >= g->n) fail(KH_EVALUE, "no such table");
+    if (G->a2a) {
+        *lo = G->blo[(size_t)rank * g->n + table];
+        *size = G->bhi[(size_t)rank * g->n + table] - *lo;
+    } else {
+        *lo = shard_lo(g->sizes[(size_t)table], G->world, rank);
+        *size = shard_lo(g->sizes[(size_t)table], G->world, rank + 1) - *lo;
+    }
+}
+int group_exchange(ShardGroup *G) { return G->a2a ? 1 : 0; }
 int group_world(ShardGroup *G) { return G->world; }
 int group_nlocal(ShardGroup *G) { return G->nlocal; }
 int group_rank(ShardGroup *G, int l) { return G->rank0 + l; }

@@ -152,6 +152,8 @@ struct Graph {
     // table (lo = 0, lsz = sizes when not sharded); nbytes are the slice's bytes
     int world = 1, rank = 0;
     bool grouped = false;             // a shard of a ShardGroup (its winners are routed by window)
+    int force_s2 = -1;                // level-2 fan-out fixed by the group (exchange mode: the
+                                      // unsharded geometry's, so level-1 buckets line up)
     std::vector<uint64_t> lo, lsz;
     Geometry geo;
     Params prm;
@@ -283,9 +285,11 @@ void engine_collect_events(Graph *g);
 struct ShardGroup;
 void group_unique_id(unsigned char *out, size_t n);
 ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank, int nlocal,
-                         const int *devices, const unsigned char *uid);
+                         const int *devices, const unsigned char *uid, int exchange);
 ShardGroup *group_create_hosted(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank,
-                                int device, const kh_transport *t);
+                                int device, const kh_transport *t, int exchange);
+void group_rank_slice(ShardGroup *G, int rank, int table, uint64_t *lo, uint64_t *size);
+int group_exchange(ShardGroup *G);
 void group_comm_info(ShardGroup *G, int *nranks, int *device);
 void group_destroy(ShardGroup *G);
 void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len);

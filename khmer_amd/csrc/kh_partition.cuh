@@ -460,7 +460,7 @@ template <class Src, int KPT, int RPT_ = L1_MAX_RPT, bool TW_ = false>
 __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) k_scatter_l1f(Params P, Src src, uint64_t nkmers, uint64_t kpw, int t0,
                                                            int nt, const uint64_t *bkt_base,
                                                            unsigned long long *bkt_cur, uint64_t *rec,
-                                                           uint64_t *ctr, int blk_sh) {
+                                                           uint64_t *ctr, int blk_sh, uint32_t jbase) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int RPT = RPT_;
     constexpr int TILE_RECS = L1_THREADS * RPT;
@@ -722,8 +722,8 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
                 const uint2 bj = sbj2[m], st = stage2[m];
                 const uint32_t d = bj.x >> 16;
                 const bool r0 = (bj.x & 0xFFFFu) != SLOT_EMPTY, r1 = (bj.y & 0xFFFFu) != SLOT_EMPTY;
-                const uint64_t v0 = ((j0 + (bj.x & 0xFFFFu)) << 32) | st.x;
-                const uint64_t v1 = ((j0 + (bj.y & 0xFFFFu)) << 32) | st.y;
+                const uint64_t v0 = ((jbase + j0 + (bj.x & 0xFFFFu)) << 32) | st.x;
+                const uint64_t v1 = ((jbase + j0 + (bj.y & 0xFFFFu)) << 32) | st.y;
                 const uint2 ql = qq[d];   // (qs, qlim): both even
                 if (P.ablate & 16) continue;   // timing only: no run writes
                 const uint64_t o = dl[2 * d + (q >= ql.x ? 1 : 0)] + q;
@@ -1290,7 +1290,7 @@ constexpr int L2F_BLK_SH = 6;   // default block: 64 records (KH_L2F_BLK_SH)
 constexpr uint64_t L2F_DEAD = ~0ull;
 
 template <int THREADS, int RPT>
-__global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, int s2, uint32_t parts,
+__global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, int s2, uint32_t parts,
                                                          const uint64_t *bstart, const uint64_t *bend,
                                                          const uint64_t *reg_base,
                                                          unsigned long long *reg_cur, const uint64_t *rec_in,
@@ -1311,13 +1311,15 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t F1, int s0, in
     // capacity with unwritten slots below it: nothing of this pass's level 1
     // may be read; the host redoes the pass on the exact path.
     if (__builtin_amdgcn_readfirstlane((uint32_t)ctr[CTR_ERR]) & 8u) return;
+    // segment b: records [bstart[b], bend[b]) of level-1 bucket b % nbk (one
+    // segment per bucket, or per (source, bucket) on an exchange-mode owner)
     const uint32_t b = blockIdx.x / parts, p = blockIdx.x % parts;
     const uint64_t b0 = bstart[b], b1 = min(bend[b], bstart[b + 1]);
     // parts of an even length: every tile starts on a 16-B record pair
     // (bucket bases are block-aligned), loaded with one 16-B load per pair
     const uint64_t len = ((b1 - b0 + parts - 1) / parts + 1) & ~1ull;
     const uint64_t r0 = min(b1, b0 + (uint64_t)p * len), r1 = min(b1, r0 + len);
-    const uint64_t gb = (uint64_t)b << s2;
+    const uint64_t gb = (uint64_t)(b % nbk) << s2;
     auto load_tile = [&](uint64_t n0, uint64_t *v) {
         const uint64_t n1 = min(r1, n0 + TILE);
 #pragma unroll

@@ -43,33 +43,46 @@ def shard_slices(sizes, world):
             for r in range(world)]
 
 
-def reinterleave(kind, p, parts):
-    """Table bytes of a p-bin table from its rank slices (in rank order).
-    Non-final Bit/Nibble slices are whole bytes followed by one spare byte."""
-    out = bytearray()
+def _slice_nbytes(kind, lo, size, p):
+    """Bytes a rank slice [lo, lo + size) of a p-bin table contributes to the
+    reference layout: whole bytes of its bins, plus the table's spare trailing
+    byte (storage.hh) on the slice that ends the table."""
+    last = size > 0 and lo + size == p
+    if kind == _lib.STORAGE_BIT:
+        return size // 8 + (1 if last else 0)
+    if kind == _lib.STORAGE_NIBBLE:
+        return size // 2 + (1 if last else 0)
+    return size
+
+
+def reinterleave(kind, p, parts, slices=None):
+    """Table bytes of a p-bin table from its rank slices (in rank order);
+    slices = [(lo, size)] per rank (default: the broadcast-mode shard_lo
+    slices).  Non-final Bit/Nibble slices are whole bytes followed by one spare
+    byte."""
     world = len(parts)
-    for r, part in enumerate(parts):
-        size = shard_lo(p, world, r + 1) - shard_lo(p, world, r)
-        if kind == _lib.STORAGE_BIT:
-            n = size // 8 + (1 if r == world - 1 else 0)
-        elif kind == _lib.STORAGE_NIBBLE:
-            n = size // 2 + (1 if r == world - 1 else 0)
-        else:
-            n = size
-        out += bytes(part[:n])
+    if slices is None:
+        slices = [(shard_lo(p, world, r), shard_lo(p, world, r + 1) - shard_lo(p, world, r)) for r in range(world)]
+    out = bytearray()
+    for part, (lo, size) in zip(parts, slices):
+        out += bytes(part[:_slice_nbytes(kind, lo, size, p)])
     return bytes(out)
 
 
-def _slice_bytes(kind, part, size, last):
-    """The bytes rank slice `part` (of `size` bins) contributes to the
-    reference layout (reinterleave, one slice at a time)."""
-    if kind == _lib.STORAGE_BIT:
-        n = size // 8 + (1 if last else 0)
-    elif kind == _lib.STORAGE_NIBBLE:
-        n = size // 2 + (1 if last else 0)
-    else:
-        n = size
-    return bytes(part[:n])
+MAX_PASS_KMERS = 3200 << 20   # kh_internal.h
+
+
+def exchange_passes(nreads, read_len, k, world, batch_kmers):
+    """[(r0, nr)]: the passes an exchange-mode group takes from every rank's
+    `nreads` reads (kh_engine.hip group_consume_a2a).  Pass p's stream is
+    reads [r0, r0 + nr) of rank 0, then of rank 1, ...; n_unique and the
+    bigcounts are exact for that order."""
+    kpr = read_len - k + 1
+    cap = min(int(batch_kmers), MAX_PASS_KMERS) // world
+    rpb0 = max(1, (cap - 16 if cap > 16 else 1) // kpr)
+    npass = max(1, -(-nreads // rpb0))
+    rpb = max(1, -(-nreads // npass))
+    return [(r0, min(rpb, nreads - r0)) for r0 in range(0, nreads, rpb)]
 
 
 def window_owner_range(fj, world, r):
@@ -191,7 +204,8 @@ class HostTransport(object):
 class ShardedGraph(object):
     """A Countgraph/Nodegraph/SmallCountgraph split over `world` ranks."""
 
-    def __init__(self, cls, k, sizes, world, rank=0, device=0, loopback=False, uid=None, transport=None):
+    def __init__(self, cls, k, sizes, world, rank=0, device=0, loopback=False, uid=None, transport=None,
+                 exchange=False):
         self._h = None
         self.shards = []
         self.kind = KIND[cls]
@@ -202,12 +216,14 @@ class ShardedGraph(object):
         devs = (ctypes.c_int * nlocal)(*([device] * nlocal))
         arr = (ctypes.c_uint64 * len(sizes))(*self.sizes)
         h = ctypes.c_void_p()
+        mode = _lib.GROUP_EXCHANGE if exchange else _lib.GROUP_BROADCAST
+        self.exchange = bool(exchange)
         if transport is not None:
-            check(lib.kh_group_create_hosted(self.kind, _lib.HASH_TWOBIT, k, arr, len(sizes), world, rank, device,
-                                             ctypes.byref(transport.struct), ctypes.byref(h)))
+            check(lib.kh_group_create_hosted_mode(self.kind, _lib.HASH_TWOBIT, k, arr, len(sizes), world, rank,
+                                                  device, ctypes.byref(transport.struct), mode, ctypes.byref(h)))
         else:
-            check(lib.kh_group_create(self.kind, _lib.HASH_TWOBIT, k, arr, len(sizes), world, rank, nlocal, devs,
-                                      uid, ctypes.byref(h)))
+            check(lib.kh_group_create_mode(self.kind, _lib.HASH_TWOBIT, k, arr, len(sizes), world, rank, nlocal,
+                                           devs, uid, mode, ctypes.byref(h)))
         self._h = h
         w, nl, r0 = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(lib.kh_group_info(h, ctypes.byref(w), ctypes.byref(nl), ctypes.byref(r0)))
@@ -243,6 +259,15 @@ class ShardedGraph(object):
         lo, n = ctypes.c_uint64(), ctypes.c_uint64()
         check(lib.kh_group_slice(self._h, l, table, ctypes.byref(lo), ctypes.byref(n)))
         return lo.value, n.value
+
+    def rank_slices(self, table):
+        """[(lo, size)] of table `table` for every rank, in rank order."""
+        out = []
+        for r in range(self.world):
+            lo, n = ctypes.c_uint64(), ctypes.c_uint64()
+            check(lib.kh_group_rank_slice(self._h, r, table, ctypes.byref(lo), ctypes.byref(n)))
+            out.append((lo.value, n.value))
+        return out
 
     def set_use_bigcount(self, flag):
         for s in self.shards:
@@ -288,7 +313,7 @@ class ShardedGraph(object):
             for i in range(len(self.sizes)):
                 for r, blob in enumerate(rdv.allgather(mine[i])):
                     parts[r].append(blob)
-        return [reinterleave(self.kind, p, [parts[r][i] for r in range(self.world)])
+        return [reinterleave(self.kind, p, [parts[r][i] for r in range(self.world)], self.rank_slices(i))
                 for i, p in enumerate(self.sizes)]
 
 
@@ -300,8 +325,10 @@ class ShardedCountgraphBench(object):
 
     def config_name(self):
         a = self.args
-        return a.graph + " k=%d %dx%.0e sharded over %dxMI355X, %d x %d bp synthetic %sreads per GPU%s" % (
-            a.k, a.tables, a.x, self.world, a.reads, a.read_len, "genomic " if a.genome else "",
+        return a.graph + " k=%d %dx%.0e sharded over %dxMI355X%s, %d x %d bp synthetic %sreads per GPU%s" % (
+            a.k, a.tables, a.x, self.world,
+            " (exchange: each rank hashes its own reads, buckets sent to owners)" if getattr(a, "exchange", False)
+            else "", a.reads, a.read_len, "genomic " if a.genome else "",
             " (strong scaling: %d reads in all)" % (a.reads * self.world) if a.strong else "")
 
     def setup(self):
@@ -314,12 +341,13 @@ class ShardedCountgraphBench(object):
         # and the rendezvous -- the dry run of several ranks on one device
         # (KH_BENCH_DEVICE), which RCCL refuses ("Duplicate GPU detected")
         self.transport = os.environ.get("KH_BENCH_TRANSPORT", "host" if "KH_BENCH_DEVICE" in os.environ else "rccl")
+        ex = bool(getattr(a, "exchange", False))
         if self.transport == "host":
             self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device,
-                                  transport=HostTransport(self.rdv))
+                                  transport=HostTransport(self.rdv), exchange=ex)
         else:
             uid = self.rdv.broadcast(ShardedGraph.unique_id() if self.rank == 0 else b"", 0)
-            self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device, uid=uid)
+            self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device, uid=uid, exchange=ex)
         nranks, dev = self.g.comm_info()
         self.comm = [tuple(int(x) for x in p.split(b",")) for p in
                      self.rdv.allgather(b"%d,%d,%d" % (self.rank, nranks, dev))]
@@ -377,11 +405,12 @@ class ShardedCountgraphBench(object):
         out = []
         for i, p in enumerate(self.sizes):
             h = hashlib.sha256() if self.rank == 0 else None
+            slices = self.g.rank_slices(i)
             for r in range(self.world):
                 blob = self.rdv.send_to_root(mine[i] if self.rank == r else b"", r)
                 if h is not None:
-                    size = shard_lo(p, self.world, r + 1) - shard_lo(p, self.world, r)
-                    h.update(_slice_bytes(self.g.kind, blob, size, r == self.world - 1))
+                    lo, size = slices[r]
+                    h.update(bytes(blob[:_slice_nbytes(self.g.kind, lo, size, p)]))
             out.append(h.hexdigest() if h is not None else None)
         return out
 

@@ -32,8 +32,8 @@ class DeviceReads(object):
         lib.kh_device_free(0, self.koff)
 
 
-def run_pair(cls, k, sizes, world, nreads, L, batch, bigcount):
-    g = parallel.ShardedGraph(cls, k, sizes, world, loopback=True)
+def run_pair(cls, k, sizes, world, nreads, L, batch, bigcount, exchange=False):
+    g = parallel.ShardedGraph(cls, k, sizes, world, loopback=True, exchange=exchange)
     g.set_batch_kmers(batch)
     o = O.Table(KIND[cls], k, sizes)
     if bigcount:
@@ -41,9 +41,16 @@ def run_pair(cls, k, sizes, world, nreads, L, batch, bigcount):
         o.set_use_bigcount(True)
     srcs = [DeviceReads(s * nreads, nreads, L, k) for s in range(world)]
     g.consume_packed_fixed_device([s.words for s in srcs], nreads, L)
-    for s in range(world):
-        seqs, offs = synth.batch(s * nreads, nreads, L)
-        o.consume_batch(seqs, [int(v) for v in offs])
+    if exchange:
+        # pass-interleaved stream: each pass holds the next chunk of every rank
+        for r0, nr in parallel.exchange_passes(nreads, L, k, world, batch):
+            for s in range(world):
+                seqs, offs = synth.batch(s * nreads + r0, nr, L)
+                o.consume_batch(seqs, [int(v) for v in offs])
+    else:
+        for s in range(world):
+            seqs, offs = synth.batch(s * nreads, nreads, L)
+            o.consume_batch(seqs, [int(v) for v in offs])
     return g, o
 
 
@@ -76,6 +83,50 @@ def test_loopback_group_saturated_bigcount(world):
     g, o = run_pair("Countgraph", 21, sizes, world, nreads=12000 // world, L=150, batch=100000, bigcount=True)
     assert len(o.bigcounts()) > 100
     assert_group_equals_oracle(g, o, sizes, True)
+    g.close()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("cls,k", [("Countgraph", 21), ("Nodegraph", 31), ("SmallCountgraph", 21)])
+def test_loopback_exchange_matches_oracle(cls, k, world):
+    """Exchange mode (Option A): every rank hashes only its own reads and sends
+    each level-1 bucket to its owner.  Several passes per call (batch below
+    the reads' k-mers), each taking the next chunk of every rank: tables,
+    counters and the replicated bigcount maps equal the oracle's over the
+    pass-interleaved stream."""
+    sizes = O.get_n_primes_near_x(4, 200003)
+    g, o = run_pair(cls, k, sizes, world, nreads=4000, L=150, batch=1 << 18, bigcount=(cls == "Countgraph"),
+                    exchange=True)
+    assert len(parallel.exchange_passes(4000, 150, k, world, 1 << 18)) > 1
+    assert_group_equals_oracle(g, o, sizes, cls == "Countgraph")
+    g.close()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_loopback_exchange_saturated_bigcount(world):
+    """Exchange mode with saturated tiny tables: crossings, full tallies merged
+    across owners, bigcount events of every rank's own k-mers replicated."""
+    sizes = O.get_n_primes_near_x(4, 3001)
+    g, o = run_pair("Countgraph", 21, sizes, world, nreads=12000 // world, L=150, batch=100000, bigcount=True,
+                    exchange=True)
+    assert len(o.bigcounts()) > 100
+    assert_group_equals_oracle(g, o, sizes, True)
+    g.close()
+
+
+def test_exchange_slices_are_bucket_ranges():
+    """Exchange-mode ownership: contiguous, covering, byte-aligned slices that
+    start on level-1 bucket boundaries (a rank may own nothing of a table)."""
+    sizes = O.get_n_primes_near_x(4, 5000011)
+    g = parallel.ShardedGraph("SmallCountgraph", 21, sizes, 3, loopback=True, exchange=True)
+    for i, p in enumerate(sizes):
+        sl = g.rank_slices(i)
+        assert sum(n for _, n in sl) == p
+        nz = [(lo, n) for lo, n in sl if n]
+        assert nz[0][0] == 0
+        for (a, n), (b, _) in zip(nz, nz[1:]):
+            assert a + n == b and b % 8 == 0
+        assert [g.slice(l, i) for l in range(3)] == sl
     g.close()
 
 

@@ -35,7 +35,8 @@ def _rank_main():
     _lib.set_default_device(0)
     rdv = Rendezvous(rank, world, "127.0.0.1", int(os.environ["KH_RDV_PORT"]), timeout=120)
     tp = parallel.HostTransport(rdv)
-    g = parallel.ShardedGraph(cfg["cls"], cfg["k"], cfg["sizes"], world, rank, 0, transport=tp)
+    g = parallel.ShardedGraph(cfg["cls"], cfg["k"], cfg["sizes"], world, rank, 0, transport=tp,
+                              exchange=cfg.get("exchange", False))
     g.set_batch_kmers(cfg["batch"])
     if cfg["bigcount"]:
         g.set_use_bigcount(True)
@@ -71,18 +72,23 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("cls,world,bigcount", [("Countgraph", 2, True), ("Countgraph", 3, True),
-                                                ("Nodegraph", 2, False), ("SmallCountgraph", 3, False)])
-def test_hosted_group_multiprocess(cls, world, bigcount):
+@pytest.mark.parametrize("cls,world,bigcount,exchange", [("Countgraph", 2, True, False), ("Countgraph", 3, True, False),
+                                                         ("Nodegraph", 2, False, False),
+                                                         ("SmallCountgraph", 3, False, False),
+                                                         ("Countgraph", 2, True, True), ("Countgraph", 3, True, True),
+                                                         ("Nodegraph", 2, False, True)])
+def test_hosted_group_multiprocess(cls, world, bigcount, exchange):
+    """exchange=True: Option A through the host transport's alltoallv (the
+    oracle consumes the pass-interleaved stream, parallel.exchange_passes)."""
     import hashlib
     from oracle import oracle as O
-    from khmer_amd import synth
+    from khmer_amd import parallel, synth
     sizes = O.get_n_primes_near_x(4, 100003)
     # bigcount cases read a 6 kbp genome (every k-mer ~400x, past 255 in all
     # tables); the others the iid stream
     genome = 6000 if bigcount else 0
     cfg = {"cls": cls, "k": 21, "sizes": sizes, "batch": 1 << 20, "bigcount": bigcount, "nreads": 20000, "L": 150,
-           "genome": genome}
+           "genome": genome, "exchange": exchange}
     port = _free_port()
     procs = []
     for r in range(world):
@@ -102,11 +108,14 @@ def test_hosted_group_multiprocess(cls, world, bigcount):
         outs.append(json.loads([ln for ln in so.splitlines() if ln.startswith("RESULT ")][-1][7:]))
     o = O.Table(KINDS[cls], 21, sizes)
     o.set_use_bigcount(bigcount)
-    for s in range(world):
+    n = cfg["nreads"]
+    order = ([(s * n + r0, nr) for r0, nr in parallel.exchange_passes(n, cfg["L"], 21, world, cfg["batch"])
+              for s in range(world)] if exchange else [(s * n, n) for s in range(world)])
+    for start, cnt in order:
         if genome:
-            seqs, offs = synth.genomic_batch(s * cfg["nreads"], cfg["nreads"], cfg["L"], genome)
+            seqs, offs = synth.genomic_batch(start, cnt, cfg["L"], genome)
         else:
-            seqs, offs = synth.batch(s * cfg["nreads"], cfg["nreads"], cfg["L"])
+            seqs, offs = synth.batch(start, cnt, cfg["L"])
         o.consume_batch(seqs, [int(v) for v in offs])
     r0 = [x for x in outs if x["rank"] == 0][0]
     assert r0["tables"] == [hashlib.sha256(o.table_bytes(i)).hexdigest() for i in range(len(sizes))]

@@ -5,7 +5,8 @@ device, device copies instead of RCCL broadcasts) over G x R synthetic reads
 (weak scaling: R reads per source rank), and prints the wall time per step
 divided by G -- the compute time one rank of a real G-GPU group spends, minus
 the broadcast -- with the per-kernel breakdown summed over shards / G.
-Usage: python tools/loopback_bench.py [world] [reads_per_rank] [steps] [batch_kmers]
+Usage: python tools/loopback_bench.py [world] [reads_per_rank] [steps] [batch_kmers] [exchange]
+(exchange = 1: Option A, kh_group_create_mode KH_GROUP_EXCHANGE)
 """
 import ctypes
 import json
@@ -21,10 +22,11 @@ from khmer_amd._lib import lib, check  # noqa: E402
 world = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 reads = int(sys.argv[2]) if len(sys.argv) > 2 else 50_000_000
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 1
-batch = int(sys.argv[4]) if len(sys.argv) > 4 else 2560 << 20
+batch = int(sys.argv[4]) if len(sys.argv) > 4 else 3200 << 20
+exchange = len(sys.argv) > 5 and sys.argv[5] == "1"
 L, k = 150, 21
 sizes = khmer_amd.get_n_primes_near_x(4, 1e9)
-g = parallel.ShardedGraph("Countgraph", k, sizes, world, loopback=True)
+g = parallel.ShardedGraph("Countgraph", k, sizes, world, loopback=True, exchange=exchange)
 g.set_use_bigcount(True)
 g.set_batch_kmers(batch)
 bufs = []
@@ -57,7 +59,7 @@ for sh in g.shards:
         name, cnt, ms = line.split("\t")
         tot[name] = tot.get(name, 0.0) + float(ms) / steps / world
 u, o = g.counters()
-print(json.dumps({"world": world, "reads_per_rank": reads, "ms_per_step_total": dt * 1e3,
+print(json.dumps({"world": world, "exchange": exchange, "reads_per_rank": reads, "ms_per_step_total": dt * 1e3,
                   "ms_per_rank_step": dt * 1e3 / world,
                   "kernels_ms_per_rank_step": {a: round(b, 2) for a, b in sorted(tot.items()) if b > 0.5},
                   "n_unique": u, "n_occupied": o}), flush=True)
