@@ -9,11 +9,14 @@ The reads are generated straight into HBM before timing
 the tables, then consume every read (hash -> partition -> LDS apply ->
 finalize), i.e. the whole hot path over the whole batch.
 
-Multi-GPU (torchrun, one rank per GPU): every table is split into G
-contiguous bin ranges, one per rank.  Every rank generates
-its own 50M reads (weak scaling); each rank's packed reads are broadcast over
-RCCL/xGMI, every rank hashes every k-mer and applies only the inserts whose
-bins it owns (Option B).  value = all ranks' k-mers / max time.
+Multi-GPU (one rank per GPU; `--gpus N` starts the N rank processes itself
+unless a launcher set WORLD_SIZE): every table is split into G contiguous bin
+ranges, one per rank.  Every rank generates its own 50M
+reads (weak scaling).  Default group mode "exchange" (Option A): each rank
+hashes only its own reads into level-1 buckets and sends every bucket to its
+owner over RCCL/xGMI (grouped send/recv); "broadcast" (Option B): each rank's
+reads are broadcast and every rank hashes every k-mer, keeping its own bins'
+updates.  value = all ranks' k-mers / max time.
 
 Prints ONE JSON line (rank 0).
 """
@@ -79,9 +82,10 @@ def parse():
                          "0 = iid uniform reads")
     ap.add_argument("--strong", action="store_true",
                     help="multi-GPU strong scaling: --reads is the whole job, split over the ranks")
-    ap.add_argument("--exchange", action="store_true",
-                    help="multi-GPU Option A: every rank hashes only its own reads and sends each level-1 bucket "
-                         "to its owner (default: Option B, read broadcast + owner-computes)")
+    ap.add_argument("--group-mode", choices=["exchange", "broadcast"], default="exchange",
+                    help="multi-GPU: 'exchange' (Option A, default: every rank hashes only its own reads and sends "
+                         "each level-1 bucket to its owner) or 'broadcast' (Option B: reads broadcast, every rank "
+                         "hashes every k-mer and keeps its own bins' updates); DESIGN.md §6")
     ap.add_argument("--query", action="store_true",
                     help="time get_median_count over the reads (tables built from them first, untimed)")
     ap.add_argument("--ablate", type=int, default=0,
@@ -100,6 +104,7 @@ def parse():
     a.bigcount = a.graph == "Countgraph" and not a.no_bigcount
     a.genome = int(a.genome)
     a.murmur = a.graph in MURMUR
+    a.exchange = a.group_mode == "exchange"
     return a
 
 

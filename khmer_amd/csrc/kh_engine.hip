@@ -2509,7 +2509,7 @@ static void group_consume_a2a(ShardGroup *G, const uint64_t *const *d_words, uin
         for (int l = 0; l < NL; l++) {
             Graph *V = G->views[l];
             KH_HIP(hipSetDevice(V->device));
-            V->use_bigcount = G->shards[l]->use_bigcount;
+            V->use_bigcount = false;   // the owners finalize; the view only runs level 1
             V->profile = G->shards[l]->profile;
             SrcTwoBit sb = src_twobit(V, d_words[l]);
             set_fixed(sb, kpr);

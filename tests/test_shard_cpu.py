@@ -107,3 +107,64 @@ def test_gloo_world2_gather(tmp_path):
     res = str(tmp_path / "res.txt")
     mp.spawn(_gloo_worker, args=(2, _free_port(), res), nprocs=2, join=True)
     assert open(res).read() == "ok"
+
+
+def _bucket_slices(p_list, world, span):
+    """Exchange-mode ownership (kh_engine.hip a2a_plan) restated: the
+    unsharded tables back to back in span-aligned ranges, F1 buckets split
+    into world contiguous ranges."""
+    tbase, acc = [], 0
+    for p in p_list:
+        tbase.append(acc)
+        acc += -(-p // span) * span
+    f1 = acc // span
+    bounds = [f1 * r // world for r in range(world + 1)]
+    out = []
+    for i, p in enumerate(p_list):
+        def bin_of(b):
+            x = b * span
+            return 0 if x <= tbase[i] else min(p, x - tbase[i])
+        out.append([(bin_of(bounds[r]), bin_of(bounds[r + 1]) - bin_of(bounds[r])) for r in range(world)])
+    return out
+
+
+@pytest.mark.parametrize("cls,kind", KINDS)
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_reinterleave_bucket_slices(cls, kind, world):
+    """Exchange-mode slices (bucket aligned; a rank may hold nothing of a
+    table, or its last bins): the generic reinterleave puts the tables back
+    together, the table's spare trailing byte taken from the slice that ends
+    the table."""
+    sizes = O.get_n_primes_near_x(3, 20011) + [13]
+    o = O.Table(kind, 12, sizes)
+    o.consume_fastx(data("test-abund-read-2.fa"))
+    slices = _bucket_slices(sizes, world, 4096)
+    for i, p in enumerate(sizes):
+        t = o.table_bytes(i)
+        parts = []
+        for lo, n in slices[i]:
+            last = n > 0 and lo + n == p
+            if kind == O.BIT:
+                parts.append(t[lo // 8: lo // 8 + n // 8 + (1 if last else 0)] + (b"" if last else b"\0"))
+            elif kind == O.NIBBLE:
+                parts.append(t[lo // 2: lo // 2 + n // 2 + (1 if last else 0)] + (b"" if last else b"\0"))
+            else:
+                parts.append(t[lo: lo + n])
+        assert parallel.reinterleave(kind, p, parts, slices[i]) == t
+
+
+@pytest.mark.parametrize("nreads,world,batch", [(4000, 2, 1 << 18), (20000, 3, 1 << 20), (7, 8, 10 ** 6),
+                                                (50_000_000, 8, 3200 << 20)])
+def test_exchange_passes_cover_reads(nreads, world, batch):
+    """parallel.exchange_passes (kh_engine.hip group_consume_a2a): the passes
+    cover every rank's reads once, in order, and a pass's k-mer index space
+    (world x the chunk's k-mers rounded up to 16) stays below the u32 limit
+    and the batch size."""
+    L, k = 150, 21
+    ps = parallel.exchange_passes(nreads, L, k, world, batch)
+    assert ps[0][0] == 0 and sum(n for _, n in ps) == nreads
+    for (a, n), (b, _) in zip(ps, ps[1:]):
+        assert a + n == b
+    kpr = L - k + 1
+    stride = max((n * kpr + 15) // 16 * 16 for _, n in ps)
+    assert world * stride <= min(batch, parallel.MAX_PASS_KMERS) or max(n for _, n in ps) == 1
