@@ -60,12 +60,15 @@ def main():
         wr.writerows(rows)
     dom = bench["roofline"]["kernel"]
     per = {timer_name(r["kernel"]): r["hbm_bytes_per_launch"] for r in rows}
+    # the bench's roofline.traffic source: the default (C2 consume) workload
+    # only; other profiles (e.g. <tag>_query) keep their csv alone
+    traffic_json = os.path.join(prof, "pmc_traffic.json" if not tag.endswith("_query") else "%s_traffic.json" % tag)
     json.dump({"kernel": dom, "config": bench["config"]["workload"],
                "hbm_bytes_per_launch": per.get(dom),
                "kernels": per,
                "note": "HBM bytes per launch (FETCH_SIZE doubled per the gfx950 calibration + WRITE_SIZE), "
                        "keyed by the engine's kernel timer names; tag %s" % tag},
-              open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+              open(traffic_json, "w"), indent=1)
     print("dominant", dom, per.get(dom))
 
 
@@ -80,7 +83,8 @@ def timer_name(device_kernel):
     if base == "apply_bit":
         return "apply_bit"
     # the fixed-capacity partitions time under the same names as the exact ones
-    return {"scatter_l1f": "scatter_l1", "scatter_l2f": "scatter_l2"}.get(base, base)
+    return {"scatter_l1f": "scatter_l1", "scatter_l2f": "scatter_l2", "hist_wf": "hist_w", "scatter_wf": "scatter_w",
+            "mark_wf": "mark", "median_fixed": "median"}.get(base, base)
 
 
 if __name__ == "__main__":
