@@ -193,3 +193,42 @@ def test_loopback_group_full_c2(world):
     finally:
         srcs = []
         g.close()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_loopback_exchange_full_c2(world):
+    """Exchange mode (Option A) at the benchmark geometry: the c2_full stream
+    split into `world` source blocks, each rank hashing only its own block
+    into the 240 unsharded level-1 buckets and sending every bucket range to
+    its owner.  The tables (re-interleaved from the bucket-aligned slices) and
+    n_occupied do not depend on the stream order and must equal the golden
+    fixture; n_unique follows the pass-interleaved order and must stay within
+    a few k-mers of the fixture's (table collisions make the count
+    order-dependent only at the margin)."""
+    import hashlib
+    from tests import full_digest as FD
+    fx = FD.load("c2_full")
+    c = fx["params"]
+    per = c["reads"] // world
+    g = parallel.ShardedGraph("Countgraph", c["k"], fx["table_sizes"], world, loopback=True, exchange=True)
+    g.set_batch_kmers(1600 << 20)   # the views' and owners' buffers of all ranks share one device
+    g.set_use_bigcount(True)
+    srcs = []
+    try:
+        for s in range(world):
+            d = DeviceReads.__new__(DeviceReads)
+            d.words, d.koff = ctypes.c_void_p(), ctypes.c_void_p()
+            check(lib.kh_device_malloc(0, (per * c["L"] // 32 + 2) * 8, ctypes.byref(d.words)))
+            check(lib.kh_device_malloc(0, (per + 1) * 8, ctypes.byref(d.koff)))
+            check(lib.kh_synth_packed_device(0, fx["seed"], s * per, per, c["L"], c["k"], d.words, d.koff))
+            srcs.append(d)
+        g.consume_packed_fixed_device([d.words for d in srcs], per, c["L"])
+        srcs = []
+        u, occ = g.counters()
+        assert occ == fx["n_occupied"]
+        assert abs(u - fx["n_unique_kmers"]) <= fx["n_unique_kmers"] // 100000
+        tabs = g.gather_tables()
+        assert [hashlib.sha256(t).hexdigest() for t in tabs] == fx["table_sha256"]
+    finally:
+        srcs = []
+        g.close()
