@@ -408,7 +408,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
                     if (t >= (uint32_t)d) incl += y;
                 }
                 cst0[t] = incl - c;
-                cgb[t] = c ? atomicAdd(&A.cw_cur[t], (unsigned long long)c) : 0ull;
+                cgb[t] = (c && !(P.ablate & 512)) ? atomicAdd(&A.cw_cur[t], (unsigned long long)c) : 0ull;   // 512: timing only
                 chist[t] = 0;   // placement cursors
             }
             block_sync();
@@ -575,7 +575,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_bit(Params P, ApplyArgs A) {
                     if (t >= (uint32_t)d) incl += y;
                 }
                 cst0[t] = incl - c;
-                cgb[t] = c ? atomicAdd(&A.cw_cur[t], (unsigned long long)c) : 0ull;
+                cgb[t] = (c && !(P.ablate & 512)) ? atomicAdd(&A.cw_cur[t], (unsigned long long)c) : 0ull;   // 512: timing only
                 chist[t] = 0;   // placement cursors
             }
             block_sync();

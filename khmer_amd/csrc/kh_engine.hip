@@ -842,6 +842,30 @@ static void pass_apply(Graph *g, PassState &ps, bool l2f) {
 template <class Src>
 static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     if (nkmers > MAX_PASS_KMERS) fail(KH_EVALUE, "device batch too large (more than 3200 * 2^20 k-mers)");
+    if constexpr (std::is_same<Src, SrcBytes>::value || std::is_same<Src, SrcTwoBit>::value) {
+        // Murmur (the costly hash) over more than 1024 level-1 buckets: the
+        // exact level 1 would hash every k-mer twice (histogram, scatter);
+        // hash once into a u64 array and run the partition over that.
+        // KH_HASH_ONCE=0 keeps the two hashings, =2 also hashes 2-bit
+        // sources once (development A/B).
+        static const int once = env_seg("KH_HASH_ONCE", 1);
+        const bool want = std::is_same<Src, SrcBytes>::value ? once != 0 : once == 2;
+        if (want && !l1f_ok(g) && !use_own_filter(g)) {
+            Workspace &w = g->ws;
+            ensure((void **)&w.frec, &w.cap_frec, nkmers, 8);
+            const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nkmers + 255) / 256, 4096));
+            TIMED("hash", hipLaunchKernelGGL(k_hash_kmers<Src>, dim3(grid), dim3(256), 0, g->stream, src, nkmers,
+                                             w.frec));
+            KH_HIP(hipGetLastError());
+            SrcHashes hs{};
+            static_cast<SrcCommon &>(hs) = static_cast<const SrcCommon &>(src);
+            hs.koff = nullptr;
+            hs.kpr = 0;
+            hs.kbase = 0;
+            hs.h = w.frec;
+            return pass_stage_a(g, hs, nkmers);
+        }
+    }
     const Params &P = g->prm;
     PassState ps;
     ps.q = pass_geo(P, nkmers);

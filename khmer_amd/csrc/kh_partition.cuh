@@ -1454,6 +1454,14 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
     }
 }
 
+// every k-mer's hash of a batch into h[0, nkmers): a Murmur batch on the exact
+// (two-pass) level 1 then reads its hashes twice instead of hashing twice
+template <class Src>
+__global__ void __launch_bounds__(256) k_hash_kmers(Src src, uint64_t nkmers, uint64_t *h) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < nkmers; j += (uint64_t)gridDim.x * blockDim.x)
+        h[j] = kmer_hash_global(src, j);
+}
+
 // per-pass region cursors start at their region bases
 __global__ void k_reg_reset(const uint64_t *reg_base, unsigned long long *reg_cur, uint64_t n) {
     for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x)
