@@ -1106,11 +1106,34 @@ __global__ void __launch_bounds__(PT_THREADS) k_mark_multi(const uint32_t *recv,
 
 // nonzero per-k-mer full tallies -> (j << 8 | tally) list (rare events)
 __global__ void k_full_compact(const uint8_t *fullf, uint64_t nkmers, uint64_t *list, uint64_t cap, uint64_t *ctr) {
-    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < nkmers; j += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t f = fullf[j];
-        if (!f) continue;
-        const uint64_t idx = atomicAdd((unsigned long long *)&ctr[CTR_NFULL], 1ull);
-        if (idx < cap) list[idx] = (j << 8) | f;   // overflow: the host sees NFULL > cap and retries
+    // one counter atomic per wave (a saturated stream makes most k-mers full)
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t n_iter = (nkmers + stride - 1) / stride;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t it = 0; it < n_iter; it++) {
+        const uint64_t j = it * stride + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+        const uint32_t f = j < nkmers ? fullf[j] : 0u;
+        const uint64_t m = __ballot(f != 0);
+        if (!m) continue;
+        uint64_t base = 0;
+        if (lane == 0) base = atomicAdd((unsigned long long *)&ctr[CTR_NFULL], (unsigned long long)__popcll(m));
+        base = __shfl(base, 0, 64);
+        const uint64_t idx = base + (uint64_t)__popcll(m & ((1ull << lane) - 1));
+        if (f && idx < cap) list[idx] = (j << 8) | f;   // overflow: the host sees NFULL > cap
+    }
+}
+
+// dst += src bytewise over n bytes (16-B aligned, n a multiple of 16); the
+// per-k-mer full tallies of all shards sum to at most N < 256, so no carries
+__global__ void k_add_bytes(uint8_t *dst, const uint8_t *src, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n / 16; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 d = ((uint4 *)dst)[i];
+        const uint4 s = ((const uint4 *)src)[i];
+        d.x += s.x;
+        d.y += s.y;
+        d.z += s.z;
+        d.w += s.w;
+        ((uint4 *)dst)[i] = d;
     }
 }
 

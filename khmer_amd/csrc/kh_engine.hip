@@ -2103,10 +2103,57 @@ static void group_route_winners(ShardGroup *G, std::vector<PassState> &ps) {
     }
 }
 
-// bigcount: per-k-mer full tallies of all shards summed on every rank
+// bigcount: per-k-mer full tallies of all shards summed on every rank.  Sparse
+// (each rank's nonzero tallies compacted and all-gathered) while the lists
+// are small; dense (the whole per-k-mer byte array summed: an RCCL uint8
+// all-reduce) when a list would outgrow FULL_LIST_CAP or the dense array --
+// a saturated stream makes most k-mers full in some table
+static void group_merge_full_dense(ShardGroup *G, uint64_t nkb) {
+    const int W = G->world, NL = G->nlocal;
+    if (G->comm) {
+        Graph *g = G->shards[0];
+        KH_HIP(hipSetDevice(g->device));
+        KH_NCCL(ncclAllReduce(g->ws.fullf, g->ws.fullf, nkb, ncclUint8, ncclSum, G->comm, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+        return;
+    }
+    if (G->hosted) {
+        Graph *g = G->shards[0];
+        KH_HIP(hipSetDevice(g->device));
+        std::vector<uint8_t> mine(nkb), all((size_t)W * nkb);
+        KH_HIP(hipMemcpyAsync(mine.data(), g->ws.fullf, nkb, hipMemcpyDeviceToHost, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+        host_rc(G->tp.allgather(G->tp.ctx, mine.data(), all.data(), nkb), "allgather");
+        for (uint64_t i = 0; i < nkb; i++) {
+            uint32_t v = 0;
+            for (int r = 0; r < W; r++) v += all[(size_t)r * nkb + i];
+            mine[i] = (uint8_t)v;
+        }
+        KH_HIP(hipMemcpyAsync(g->ws.fullf, mine.data(), nkb, hipMemcpyHostToDevice, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+        return;
+    }
+    // loopback: sum every shard's array into shard 0's, then copy it back out
+    Graph *g0 = G->shards[0];
+    KH_HIP(hipSetDevice(g0->device));
+    for (int l = 0; l < NL; l++) KH_HIP(hipStreamSynchronize(G->shards[l]->stream));
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nkb / 16 / 256 + 1, 4096));
+    uint8_t *tmp = nullptr;
+    KH_HIP(hipMalloc((void **)&tmp, nkb + 64));
+    for (int l = 1; l < NL; l++) {
+        KH_HIP(hipMemcpyAsync(tmp, G->shards[l]->ws.fullf, nkb, hipMemcpyDefault, g0->stream));
+        hipLaunchKernelGGL(k_add_bytes, dim3(grid), dim3(256), 0, g0->stream, g0->ws.fullf, tmp, nkb);
+    }
+    KH_HIP(hipStreamSynchronize(g0->stream));
+    KH_HIP(hipFree(tmp));
+    for (int l = 1; l < NL; l++)
+        KH_HIP(hipMemcpy(G->shards[l]->ws.fullf, g0->ws.fullf, nkb, hipMemcpyDefault));
+    KH_HIP(hipGetLastError());
+}
+
 static void group_merge_full(ShardGroup *G, std::vector<PassState> &ps) {
     const int W = G->world, NL = G->nlocal;
-    const uint64_t nk = ps[0].nkmers;
+    const uint64_t nk = ps[0].nkmers, nkb = (nk + 15) & ~15ull;
     std::vector<uint64_t> cnt(W, 0);
     for (int l = 0; l < NL; l++) {
         Graph *g = G->shards[l];
@@ -2114,57 +2161,60 @@ static void group_merge_full(ShardGroup *G, std::vector<PassState> &ps) {
         KH_HIP(hipSetDevice(g->device));
         ensure((void **)&lc.flist, &lc.cap_flist, 1024, 8);
         const uint64_t cap = std::min<uint64_t>(FULL_LIST_CAP, lc.cap_flist);
+        KH_HIP(hipMemsetAsync(g->ws.ctr + CTR_NFULL, 0, 8, g->stream));
         hipLaunchKernelGGL(k_full_compact, dim3(2048), dim3(256), 0, g->stream, g->ws.fullf, nk, lc.flist, cap,
                            g->ws.ctr);
         uint64_t h[CTR_N];
         KH_HIP(hipMemcpyAsync(h, g->ws.ctr, CTR_N * 8, hipMemcpyDeviceToHost, g->stream));
         KH_HIP(hipStreamSynchronize(g->stream));
-        if (h[CTR_NFULL] > cap) {
-            // grow once and recompute (bounded by FULL_LIST_CAP)
-            if (h[CTR_NFULL] > FULL_LIST_CAP)
-                fail(KH_EDEVICE, "too many bigcount events in one sharded batch; lower the batch size");
-            ensure((void **)&lc.flist, &lc.cap_flist, h[CTR_NFULL], 8);
-            KH_HIP(hipMemsetAsync(g->ws.ctr + CTR_NFULL, 0, 8, g->stream));
-            hipLaunchKernelGGL(k_full_compact, dim3(2048), dim3(256), 0, g->stream, g->ws.fullf, nk, lc.flist,
-                               lc.cap_flist, g->ws.ctr);
-            KH_HIP(hipStreamSynchronize(g->stream));
-        }
         cnt[G->rank0 + l] = h[CTR_NFULL];
     }
     if (per_rank(G)) {
         Graph *g = G->shards[0];
-        auto &lc = G->loc[0];
+        KH_HIP(hipSetDevice(g->device));
         KH_HIP(hipMemcpyAsync(G->d_red + 128, &cnt[G->rank0], 8, hipMemcpyHostToDevice, g->stream));
         coll_allgather_u64(G, g->stream, G->d_red + 128, G->d_red, 1);
         KH_HIP(hipMemcpyAsync(cnt.data(), G->d_red, W * 8, hipMemcpyDeviceToHost, g->stream));
         KH_HIP(hipStreamSynchronize(g->stream));
-        const uint64_t mx = *std::max_element(cnt.begin(), cnt.end());
-        if (!mx) return;
-        if (mx > lc.cap_flist) {   // grow keeping the compacted entries
-            uint64_t *nl = nullptr;
-            KH_HIP(hipMalloc((void **)&nl, mx * 8 + 64));
-            if (cnt[G->rank0])
-                KH_HIP(hipMemcpyAsync(nl, lc.flist, cnt[G->rank0] * 8, hipMemcpyDeviceToDevice, g->stream));
-            KH_HIP(hipStreamSynchronize(g->stream));
-            KH_HIP(hipFree(lc.flist));
-            lc.flist = nl;
-            lc.cap_flist = mx;
+    }
+    const uint64_t mx = *std::max_element(cnt.begin(), cnt.end());
+    if (!mx) return;
+    if (mx > FULL_LIST_CAP || mx * 8 > nkb) {   // every rank decides alike (same counts)
+        group_merge_full_dense(G, nkb);
+        return;
+    }
+    // sparse: every list complete (re-compacted into a larger list if its first
+    // buffer was short), padded to the longest, gathered and scattered back
+    for (int l = 0; l < NL; l++) {
+        Graph *g = G->shards[l];
+        auto &lc = G->loc[l];
+        const uint64_t c = cnt[G->rank0 + l];
+        KH_HIP(hipSetDevice(g->device));
+        if (c > lc.cap_flist || mx > lc.cap_flist) {
+            if (lc.flist) KH_HIP(hipFree(lc.flist));
+            lc.flist = nullptr;
+            lc.cap_flist = 0;
+            ensure((void **)&lc.flist, &lc.cap_flist, mx, 8);
+            KH_HIP(hipMemsetAsync(g->ws.ctr + CTR_NFULL, 0, 8, g->stream));
+            hipLaunchKernelGGL(k_full_compact, dim3(2048), dim3(256), 0, g->stream, g->ws.fullf, nk, lc.flist,
+                               lc.cap_flist, g->ws.ctr);
         }
-        if (mx > cnt[G->rank0])
-            KH_HIP(hipMemsetAsync(lc.flist + cnt[G->rank0], 0xFF, (mx - cnt[G->rank0]) * 8, g->stream));
+        if (mx > c) KH_HIP(hipMemsetAsync(lc.flist + c, 0xFF, (mx - c) * 8, g->stream));
+    }
+    if (per_rank(G)) {
+        Graph *g = G->shards[0];
+        auto &lc = G->loc[0];
         ensure((void **)&lc.fall, &lc.cap_fall, (uint64_t)W * mx, 8);
         coll_allgather_u64(G, g->stream, lc.flist, lc.fall, mx);
-        KH_HIP(hipMemsetAsync(g->ws.fullf, 0, (nk + 15) & ~15ull, g->stream));
+        KH_HIP(hipMemsetAsync(g->ws.fullf, 0, nkb, g->stream));
         hipLaunchKernelGGL(k_full_scatter, dim3(2048), dim3(256), 0, g->stream, lc.fall, (uint64_t)W * mx,
                            g->ws.fullf);
     } else {
-        uint64_t any = 0;
-        for (uint64_t c : cnt) any |= c;
-        if (!any) return;
+        for (int l = 0; l < NL; l++) KH_HIP(hipStreamSynchronize(G->shards[l]->stream));
         for (int l = 0; l < NL; l++) {
             Graph *g = G->shards[l];
             KH_HIP(hipSetDevice(g->device));
-            KH_HIP(hipMemsetAsync(g->ws.fullf, 0, (nk + 15) & ~15ull, g->stream));
+            KH_HIP(hipMemsetAsync(g->ws.fullf, 0, nkb, g->stream));
             for (int s = 0; s < W; s++)
                 if (cnt[s])
                     hipLaunchKernelGGL(k_full_scatter, dim3(2048), dim3(256), 0, g->stream, G->loc[s].flist, cnt[s],

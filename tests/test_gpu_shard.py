@@ -232,3 +232,44 @@ def test_loopback_exchange_full_c2(world):
     finally:
         srcs = []
         g.close()
+
+
+@pytest.mark.parametrize("exchange", [False, True])
+def test_loopback_genomic_c2(exchange):
+    """The skewed genomic_c2 stream (10M reads of a 2e6-base genome: every
+    k-mer ~500x, saturated bins, bigcounts) split over two loopback ranks.
+    Broadcast mode consumes the fixture's own order: every counter, table and
+    the bigcount map digest must match.  Exchange mode's stream is
+    pass-interleaved: tables and n_occupied (order-free) must match."""
+    import hashlib
+    from tests import full_digest as FD
+    fx = FD.load("genomic_c2")
+    c = fx["params"]
+    world = 2
+    per = c["reads"] // world
+    g = parallel.ShardedGraph("Countgraph", c["k"], fx["table_sizes"], world, loopback=True, exchange=exchange)
+    g.set_batch_kmers(c["batch_kmers"])
+    g.set_use_bigcount(True)
+    srcs = []
+    try:
+        for s in range(world):
+            d = DeviceReads.__new__(DeviceReads)
+            d.words, d.koff = ctypes.c_void_p(), ctypes.c_void_p()
+            check(lib.kh_device_malloc(0, (per * c["L"] // 32 + 2) * 8, ctypes.byref(d.words)))
+            check(lib.kh_device_malloc(0, (per + 1) * 8, ctypes.byref(d.koff)))
+            check(lib.kh_synth_genomic_device(0, fx["seed"], c["genome"], s * per, per, c["L"], c["k"], d.words,
+                                              d.koff))
+            srcs.append(d)
+        g.consume_packed_fixed_device([d.words for d in srcs], per, c["L"])
+        srcs = []
+        u, occ = g.counters()
+        assert occ == fx["n_occupied"]
+        tabs = g.gather_tables()
+        assert [hashlib.sha256(t).hexdigest() for t in tabs] == fx["table_sha256"]
+        if not exchange:
+            assert u == fx["n_unique_kmers"]
+            for sh in g.shards:   # replicated on every rank
+                assert FD.bigcount_digest(dict(sh.bigcounts())) == (fx["n_bigcounts"], fx["bigcount_sha256"])
+    finally:
+        srcs = []
+        g.close()
