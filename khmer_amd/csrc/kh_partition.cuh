@@ -629,18 +629,25 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             if (d0 < F1) lstart[d0] = acc;
             if (d0 + 1 < F1) lstart[d0 + 1] = acc + r0;
         } else if (threadIdx.x < 64) {
+            // <= 4 buckets a lane, unrolled: the lane's LDS reads issue back
+            // to back and the run sizes stay in registers for the writes
             const uint32_t lane = threadIdx.x, per = (F1 + 63) / 64, b0 = lane * per;
-            uint32_t sum = 0;
-            for (uint32_t t = 0; t < per && b0 + t < F1; t++) sum += run(b0 + t);
+            uint32_t rs[4], sum = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < 4; t++) {
+                rs[t] = (t < per && b0 + t < F1) ? run(b0 + t) : 0u;
+                sum += rs[t];
+            }
             uint32_t incl = sum;
             for (int dd = 1; dd < 64; dd <<= 1) {
                 const uint32_t y = __shfl_up(incl, dd, 64);
                 if (lane >= (uint32_t)dd) incl += y;
             }
             uint32_t acc = incl - sum;
-            for (uint32_t t = 0; t < per && b0 + t < F1; t++) {
-                lstart[b0 + t] = acc;
-                acc += run(b0 + t);
+#pragma unroll
+            for (uint32_t t = 0; t < 4; t++) {
+                if (t < per && b0 + t < F1) lstart[b0 + t] = acc;
+                acc += rs[t];
             }
         }
         block_sync();
