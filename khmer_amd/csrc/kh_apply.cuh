@@ -189,6 +189,11 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
     uint32_t *s_flag = full255 + R / 32;  // [4]
     uint8_t *c0 = (uint8_t *)(s_flag + 4);  // [R]
     uint8_t *wflag = c0 + R;              // [R/4] winner bits of each 4-bin group
+    // coarse-window winners: per-window counts then cursors, first staging
+    // slots, output bases (own arrays, cleared with the region's state)
+    uint32_t *chist = (uint32_t *)(wflag + R / 4);         // [MAX_CW]
+    uint32_t *cst0 = chist + MAX_CW;                        // [MAX_CW]
+    unsigned long long *cgb = (unsigned long long *)(cst0 + MAX_CW);   // [MAX_CW]
     const uint32_t MAXC = KIND == BYTE ? 255u : 15u;
     const bool bigc = KIND == BYTE && P.use_bigcount;
     const uint32_t t = threadIdx.x;
@@ -197,7 +202,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
     Prefetch cur, nxt;
     prefetch_region<KIND, TH>(P, A, blockIdx.x, total, load_bounds(P, A, blockIdx.x, total), cur);
     Bounds bnext = load_bounds(P, A, blockIdx.x + gridDim.x, total);
-    PH_BEGIN(6);
+    PH_BEGIN(8);
     for (uint64_t rr = blockIdx.x; rr < total; rr += gridDim.x) {
         const RegionInfo ri = cur.ri;
         if (ri.e0 == ri.e1) {
@@ -239,6 +244,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
             for (uint32_t x = t; x < R / 32; x += blockDim.x) full255[x] = 0;
             if (t == 0) s_flag[0] = s_flag[1] = 0;
         }
+        if (t < MAX_CW) chist[t] = 0;
         PH(5);
         block_sync();
         PH(0);
@@ -378,14 +384,8 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
             // coarse-window runs: per-window counts (LDS atomics), a wave-0
             // scan and one returning global atomic per non-empty window, the
             // winners placed window by window in LDS (the dead count array),
-            // then every run written by consecutive lanes.  full255 (bigcount
-            // bookkeeping, read above) holds the window counters.
-            uint32_t *chist = full255, *cst0 = full255 + MAX_CW;
-            unsigned long long *cgb = (unsigned long long *)(full255 + 2 * MAX_CW);
+            // then every run written by consecutive lanes
             const int cjs = A.cjs;
-            block_sync();   // full255's last readers (the loop above) are done
-            if (t < MAX_CW) chist[t] = 0;
-            block_sync();
             if (nw) {
 #pragma unroll
                 for (int step = 0; step < BPT / 4; step++) {
@@ -400,6 +400,11 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
                 }
             }
             block_sync();
+            PH(6);
+            // wave 0: window starts in the staging array, and the windows'
+            // output ranges reserved -- the returning atomics complete while
+            // every wave places its winners; their results go to LDS after
+            unsigned long long my_gb = 0;
             if (t < 64) {
                 const uint32_t c = chist[t];
                 uint32_t incl = c;
@@ -408,10 +413,11 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
                     if (t >= (uint32_t)d) incl += y;
                 }
                 cst0[t] = incl - c;
-                cgb[t] = (c && !(P.ablate & 512)) ? atomicAdd(&A.cw_cur[t], (unsigned long long)c) : 0ull;   // 512: timing only
+                if (c && !(P.ablate & 512)) my_gb = atomicAdd(&A.cw_cur[t], (unsigned long long)c);   // 512: timing only
                 chist[t] = 0;   // placement cursors
             }
             block_sync();
+            PH(7);
             if (nw) {
 #pragma unroll
                 for (int step = 0; step < BPT / 4; step++) {
@@ -429,6 +435,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
                 }
             }
             if (t == 0) A.wcnt[rr] = wall;
+            if (t < 64) cgb[t] = my_gb;
             block_sync();
             for (uint32_t x = t; x < wall; x += TH) {
                 const uint32_t v = wst[x], c = v >> cjs;
@@ -463,7 +470,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
         PH(3);
         cur = nxt;
     }
-    PH_END(16, 6);
+    PH_END(16, 8);
     occ = wave_sum(occ);
     if ((threadIdx.x & 63) == 0 && occ) atomicAdd((unsigned long long *)&A.ctr[CTR_OCC], (unsigned long long)occ);
 }

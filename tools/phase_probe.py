@@ -13,8 +13,8 @@ from khmer_amd._lib import lib, check  # noqa: E402
 
 PHASES = {
     "scatter_l1 (exact)": (8, ["tile top", "hash+rank", "scan", "stage", "tails", "write"]),
-    "apply": (16, ["init barrier", "records+barrier", "winner scan+barrier", "write-back+winners", "pass 1",
-                   "init"]),
+    "apply": (16, ["init barrier", "records+barrier", "winner scan+barrier", "place+write winners", "pass 1",
+                   "init", "prefetch+write-back+count", "scan+reserve"]),
     "scatter_l1f": (24, ["hash+rank", "barrier 1", "starts+scan", "stage", "reserve", "barrier 2", "write-out",
                          "advance+top barrier"]),
     "scatter_l2f": (32, ["wait+rank", "prefetch+barrier", "reserve+flist", "barrier", "flush", "barrier",
