@@ -194,6 +194,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
     uint32_t *chist = (uint32_t *)(wflag + R / 4);         // [MAX_CW]
     uint32_t *cst0 = chist + MAX_CW;                        // [MAX_CW]
     unsigned long long *cgb = (unsigned long long *)(cst0 + MAX_CW);   // [MAX_CW]
+    uint32_t *ccur = (uint32_t *)(cgb + MAX_CW);           // [MAX_CW] placement cursors
     const uint32_t MAXC = KIND == BYTE ? 255u : 15u;
     const bool bigc = KIND == BYTE && P.use_bigcount;
     const uint32_t t = threadIdx.x;
@@ -244,7 +245,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
             for (uint32_t x = t; x < R / 32; x += blockDim.x) full255[x] = 0;
             if (t == 0) s_flag[0] = s_flag[1] = 0;
         }
-        if (t < MAX_CW) chist[t] = 0;
+        if (t < MAX_CW) chist[t] = ccur[t] = 0;
         PH(5);
         block_sync();
         PH(0);
@@ -336,55 +337,49 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
         }
         if (P.ablate & 1) nw = 0;
         PH(4);
-        const uint32_t wex = wave_winner_scan(nw, s_wt);
-        block_sync();
-        PH(2);
-        if (bigc && t == 0 && s_flag[1]) {
-            const uint64_t seg = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
-            A.xseg[seg] = make_uint4((uint32_t)ri.e0, (uint32_t)(ri.e0 >> 32), (uint32_t)(ri.e1 - ri.e0), s_flag[1]);
-        }
-        prefetch_region<KIND, TH>(P, A, rr + gridDim.x, total, bnext, nxt);
-        bnext = bafter;
-        // pass 2: write back changed 16-bin chunks; winners to the region's segment
-        for (uint32_t x = t; x < nchunk; x += blockDim.x) {
-            if (!((chg[x >> 5] >> (x & 31)) & 1) || (P.ablate & 4)) continue;
-            const uint4 cv = ((const uint4 *)c0)[x];
-            if (KIND == BYTE) {
-                ((uint4 *)(tab + ri.bin_lo))[x] = cv;
-            } else {
-                // even bin -> high nibble (storage.hh:262-272)
-                const uint8_t *fin = (const uint8_t *)&cv;
-                uint2 o;
-                uint32_t *ow = (uint32_t *)&o;
+        // changed 16-bin chunks back to the table; the rare full255 re-read
+        auto write_back = [&]() {
+            // pass 2: write back changed 16-bin chunks; winners to the region's segment
+            for (uint32_t x = t; x < nchunk; x += blockDim.x) {
+                if (!((chg[x >> 5] >> (x & 31)) & 1) || (P.ablate & 4)) continue;
+                const uint4 cv = ((const uint4 *)c0)[x];
+                if (KIND == BYTE) {
+                    ((uint4 *)(tab + ri.bin_lo))[x] = cv;
+                } else {
+                    // even bin -> high nibble (storage.hh:262-272)
+                    const uint8_t *fin = (const uint8_t *)&cv;
+                    uint2 o;
+                    uint32_t *ow = (uint32_t *)&o;
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    uint32_t w = 0;
+                    for (int h = 0; h < 2; h++) {
+                        uint32_t w = 0;
 #pragma unroll
-                    for (int b = 0; b < 4; b++)
-                        w |= (uint32_t)((fin[8 * h + 2 * b] << 4) | fin[8 * h + 2 * b + 1]) << (8 * b);
-                    ow[h] = w;
+                        for (int b = 0; b < 4; b++)
+                            w |= (uint32_t)((fin[8 * h + 2 * b] << 4) | fin[8 * h + 2 * b + 1]) << (8 * b);
+                        ow[h] = w;
+                    }
+                    ((uint2 *)(tab + (ri.bin_lo >> 1)))[x] = o;
                 }
-                ((uint2 *)(tab + (ri.bin_lo >> 1)))[x] = o;
             }
-        }
-        if (bigc && s_flag[0]) {
-            // bins at 255 before the batch: every insert is "full"
-            // (ByteStorage::add, storage.hh:590-603); rare, so the region's
-            // records are read again
-            for (uint64_t q = ri.e0 + t; q < ri.e1; q += TH) {
-                const uint64_t x = A.rec[q];
-                const uint32_t o = (uint32_t)x;
-                if (x != ~0ull && ((full255[o >> 5] >> (o & 31)) & 1)) full_add(A.fullf, (uint32_t)(x >> 32));
+            if (bigc && s_flag[0]) {
+                // bins at 255 before the batch: every insert is "full"
+                // (ByteStorage::add, storage.hh:590-603); rare, so the region's
+                // records are read again
+                for (uint64_t q = ri.e0 + t; q < ri.e1; q += TH) {
+                    const uint64_t x = A.rec[q];
+                    const uint32_t o = (uint32_t)x;
+                    if (x != ~0ull && ((full255[o >> 5] >> (o & 31)) & 1)) full_add(A.fullf, (uint32_t)(x >> 32));
+                }
             }
-        }
-        uint32_t wall;
-        uint32_t pos = winner_base(s_wt, &wall) + wex;
-        uint32_t *wst = cnt;
+        };
         if (A.coarse) {
-            // coarse-window runs: per-window counts (LDS atomics), a wave-0
-            // scan and one returning global atomic per non-empty window, the
-            // winners placed window by window in LDS (the dead count array),
-            // then every run written by consecutive lanes
+            // Coarse-window runs.  The count loop reads only this thread's own
+            // pass-1 results (its wflag groups and minj bins), so one barrier
+            // publishes the counts and pass 1 (c0, chg, flags) together; every
+            // wave then scans the window counts itself (lane c: window c) and
+            // places its winners in LDS (the dead count array) without another
+            // barrier; wave 0's returning reservation atomics complete
+            // meanwhile; consecutive lanes write the runs.
             const int cjs = A.cjs;
             if (nw) {
 #pragma unroll
@@ -400,42 +395,48 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
                 }
             }
             block_sync();
-            PH(6);
-            // wave 0: window starts in the staging array, and the windows'
-            // output ranges reserved -- the returning atomics complete while
-            // every wave places its winners; their results go to LDS after
-            unsigned long long my_gb = 0;
-            if (t < 64) {
-                const uint32_t c = chist[t];
-                uint32_t incl = c;
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_up(incl, d, 64);
-                    if (t >= (uint32_t)d) incl += y;
-                }
-                cst0[t] = incl - c;
-                if (c && !(P.ablate & 512)) my_gb = atomicAdd(&A.cw_cur[t], (unsigned long long)c);   // 512: timing only
-                chist[t] = 0;   // placement cursors
+            PH(2);
+            if (bigc && t == 0 && s_flag[1]) {
+                const uint64_t seg = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
+                A.xseg[seg] = make_uint4((uint32_t)ri.e0, (uint32_t)(ri.e0 >> 32), (uint32_t)(ri.e1 - ri.e0), s_flag[1]);
             }
-            block_sync();
+            prefetch_region<KIND, TH>(P, A, rr + gridDim.x, total, bnext, nxt);
+            bnext = bafter;
+            write_back();
+            PH(6);
+            const uint32_t lane = t & 63;
+            const uint32_t cc = chist[lane];
+            uint32_t incl = cc;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(incl, d, 64);
+                if (lane >= (uint32_t)d) incl += y;
+            }
+            const uint32_t st0 = incl - cc;
+            const uint32_t wall = __shfl(incl, 63, 64);
+            unsigned long long my_gb = 0;
+            if (t < 64 && cc && !(P.ablate & 512)) my_gb = atomicAdd(&A.cw_cur[t], (unsigned long long)cc);   // 512: timing only
             PH(7);
-            if (nw) {
+            uint32_t *wst = cnt;
 #pragma unroll
-                for (int step = 0; step < BPT / 4; step++) {
-                    const uint32_t g = t + (uint32_t)step * TH;
-                    const uint32_t win = wflag[g];
-                    if (!win) continue;
-                    const uint4 m = ((const uint4 *)minj)[g];
-                    const uint32_t mv[4] = {m.x, m.y, m.z, m.w};
+            for (int step = 0; step < BPT / 4; step++) {
+                const uint32_t g = t + (uint32_t)step * TH;
+                const uint32_t win = wflag[g];
+                if (!__ballot(win != 0)) continue;   // wave-uniform: the shuffles below need every lane
+                const uint4 m = ((const uint4 *)minj)[g];
+                const uint32_t mv[4] = {m.x, m.y, m.z, m.w};
 #pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        if (win & (1u << k)) {
-                            const uint32_t c = mv[k] >> cjs;
-                            wst[cst0[c] + atomicAdd(&chist[c], 1u)] = mv[k];
-                        }
+                for (int k = 0; k < 4; k++) {
+                    const bool ok = (win >> k) & 1u;
+                    const uint32_t c = ok ? mv[k] >> cjs : 0u;
+                    const uint32_t base = __shfl(st0, (int)c, 64);
+                    if (ok) wst[base + atomicAdd(&ccur[c], 1u)] = mv[k];
                 }
             }
             if (t == 0) A.wcnt[rr] = wall;
-            if (t < 64) cgb[t] = my_gb;
+            if (t < 64) {
+                cgb[t] = my_gb;
+                cst0[t] = st0;
+            }
             block_sync();
             for (uint32_t x = t; x < wall; x += TH) {
                 const uint32_t v = wst[x], c = v >> cjs;
@@ -446,6 +447,19 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
             cur = nxt;
             continue;
         }
+        const uint32_t wex = wave_winner_scan(nw, s_wt);
+        block_sync();
+        PH(2);
+        if (bigc && t == 0 && s_flag[1]) {
+            const uint64_t seg = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
+            A.xseg[seg] = make_uint4((uint32_t)ri.e0, (uint32_t)(ri.e0 >> 32), (uint32_t)(ri.e1 - ri.e0), s_flag[1]);
+        }
+        prefetch_region<KIND, TH>(P, A, rr + gridDim.x, total, bnext, nxt);
+        bnext = bafter;
+        write_back();
+        uint32_t wall;
+        uint32_t pos = winner_base(s_wt, &wall) + wex;
+        uint32_t *wst = cnt;
         // winners: staged in LDS in region order (the count array is dead
         // after pass 1), then written to the region's segment by consecutive
         // lanes -- coalesced, where each lane writing its own run directly
@@ -492,7 +506,8 @@ __global__ void __launch_bounds__(TH, 4) k_apply_bit(Params P, ApplyArgs A) {
     uint32_t *chist = bits32 + R / 32;          // [MAX_CW] coarse windows: counts, then cursors
     uint32_t *cst0 = chist + MAX_CW;            // [MAX_CW] window's first staging slot
     unsigned long long *cgb = (unsigned long long *)(cst0 + MAX_CW);   // [MAX_CW] window's output base
-    uint32_t *wst = (uint32_t *)(cgb + MAX_CW);   // [R] winners in window order (coarse only)
+    uint32_t *ccur = (uint32_t *)(cgb + MAX_CW);           // [MAX_CW] placement cursors
+    uint32_t *wst = ccur + MAX_CW;                          // [R] winners in window order (coarse only)
     const uint32_t t = threadIdx.x;
     uint64_t occ = 0;
     const uint64_t total = A.rprefix[P.n];
@@ -514,7 +529,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_bit(Params P, ApplyArgs A) {
         if (t < nchunk) ((uint4 *)bits)[t] = cur.tv;
         for (uint32_t x = t; x < nchunk * 32; x += blockDim.x) ((uint4 *)minj)[x] = make_uint4(NO_J, NO_J, NO_J, NO_J);
         if (t < 4) chg[t] = 0;
-        if (t < MAX_CW) chist[t] = 0;
+        if (t < MAX_CW) chist[t] = ccur[t] = 0;
         block_sync();
         {
             const uint64_t step = (uint64_t)(APPLY_RECS / 2) * TH;   // pairs
@@ -574,28 +589,29 @@ __global__ void __launch_bounds__(TH, 4) k_apply_bit(Params P, ApplyArgs A) {
         uint64_t pos = ri.e0 + winner_base(s_wt, &wall) + wex;
         if (t == 0) A.wcnt[rr] = wall;
         if (A.coarse) {
-            if (t < 64) {
-                const uint32_t c = chist[t];
-                uint32_t incl = c;
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_up(incl, d, 64);
-                    if (t >= (uint32_t)d) incl += y;
-                }
-                cst0[t] = incl - c;
-                cgb[t] = (c && !(P.ablate & 512)) ? atomicAdd(&A.cw_cur[t], (unsigned long long)c) : 0ull;   // 512: timing only
-                chist[t] = 0;   // placement cursors
+            // every wave scans the window counts itself (lane c: window c) and
+            // places its winners without another barrier (as k_apply_count)
+            const uint32_t cc = chist[lane];
+            uint32_t incl = cc;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(incl, d, 64);
+                if (lane >= (uint32_t)d) incl += y;
             }
-            block_sync();
-            if (nw) {
+            const uint32_t st0 = incl - cc;
+            unsigned long long my_gb = 0;
+            if (t < 64 && cc && !(P.ablate & 512)) my_gb = atomicAdd(&A.cw_cur[t], (unsigned long long)cc);   // 512: timing only
 #pragma unroll 2
-                for (int u = 0; u < BPT; u++) {
-                    const uint32_t o = t + (uint32_t)u * TH;
-                    const uint32_t m = o < nb ? minj[o] : NO_J;
-                    if (m != NO_J) {
-                        const uint32_t c = m >> cjs;
-                        wst[cst0[c] + atomicAdd(&chist[c], 1u)] = m;
-                    }
-                }
+            for (int u = 0; u < BPT; u++) {
+                const uint32_t o = t + (uint32_t)u * TH;
+                const uint32_t m = o < nb ? minj[o] : NO_J;
+                const bool ok = m != NO_J;
+                const uint32_t c = ok ? m >> cjs : 0u;
+                const uint32_t base = __shfl(st0, (int)c, 64);
+                if (ok) wst[base + atomicAdd(&ccur[c], 1u)] = m;
+            }
+            if (t < 64) {
+                cgb[t] = my_gb;
+                cst0[t] = st0;
             }
             block_sync();
             for (uint32_t x = t; x < wall; x += TH) {

@@ -601,8 +601,8 @@ static unsigned agrid_count(const Graph *g, const PassGeo &q) {
 static size_t lds_apply(const Params &P, bool coarse = false) {
     const size_t R = (size_t)1 << P.s0;
     if (P.kind == BIT)   // coarse-window winners: window arrays + a winner staging array
-        return R * 4 + 16 + 64 + R / 8 + (coarse ? MAX_CW * 16 + R * 4 : 0);
-    return R * 4 * 2 + (R / 512) * 4 + 64 + R / 8 + 16 + R + R / 4 + MAX_CW * 16;
+        return R * 4 + 16 + 64 + R / 8 + (coarse ? MAX_CW * 20 + R * 4 : 0);
+    return R * 4 * 2 + (R / 512) * 4 + 64 + R / 8 + 16 + R + R / 4 + MAX_CW * 20;
 }
 
 // A shard's level 1 through k_own_filter (kh_partition.cuh) when it owns a
