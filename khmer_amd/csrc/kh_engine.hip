@@ -284,6 +284,12 @@ static uint32_t device_cus(const Graph *g) {
 // records per thread and tile: 8 (3 workgroups per CU; 16 records with 2
 // workgroups per CU measured slower, 117 vs 112 ms/step, round 2)
 static int l1f_rpt() { return L1_MAX_RPT; }
+// tables per k_scatter_l1f launch (development A/B: fewer tables per launch
+// means fewer live buckets and longer runs per tile, at one k-mer hash per launch)
+static int l1f_tables_per_launch() {
+    static const int v = std::max(1, std::min(L1_MAX_RPT, env_seg("KH_L1_NT", L1_MAX_RPT)));
+    return v;
+}
 static size_t lds_scatter_l1f(const Params &P, bool window, int tile_kmers) {
     const size_t F1a = (P.F1 + 3) & ~3u;
     const size_t tile = (size_t)L1_THREADS * l1f_rpt();
@@ -926,8 +932,9 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
             hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)((F1 + 255) / 256)), dim3(256), 0, st, w.bkt_base,
                                (unsigned long long *)w.bkt_cur, (uint64_t)F1);
             const uint32_t nwg = l1f_workgroups(g, nkmers);
-            for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
-                const int nt = std::min(L1_MAX_RPT, P.n - t0);
+            const int tpl = l1f_tables_per_launch();
+            for (int t0 = 0; t0 < P.n; t0 += tpl) {
+                const int nt = std::min(tpl, P.n - t0);
                 const int rpt = l1f_rpt();
                 int kpt = 1;
                 while (kpt * 2 * nt <= rpt) kpt *= 2;

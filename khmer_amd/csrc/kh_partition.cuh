@@ -30,7 +30,14 @@ __device__ unsigned long long g_dbg[64];   // development phase counters (tools/
 #define PH_BEGIN(n) uint64_t ph_[n] = {}; uint64_t phA_ = __builtin_amdgcn_s_memtime(), phB_
 #define PH(i) do { phB_ = __builtin_amdgcn_s_memtime(); ph_[i] += phB_ - phA_; phA_ = phB_; } while (0)
 #define PH_END(base, n) do { if (threadIdx.x == 0) for (int z_ = 0; z_ < (n); z_++) atomicAdd(&g_dbg[(base) + z_], (unsigned long long)ph_[z_]); } while (0)
+// PH_WG_BEGIN / PH_WG_END(base): a workgroup's wall time (100 MHz clock):
+// g_dbg[base] sum, g_dbg[base + 1] max, g_dbg[base + 2] workgroups
+#define PH_WG_BEGIN const uint64_t wg0_ = __builtin_amdgcn_s_memrealtime()
+#define PH_WG_END(base) do { if (threadIdx.x == 0) { const unsigned long long d_ = __builtin_amdgcn_s_memrealtime() - wg0_; \
+    atomicAdd(&g_dbg[(base)], d_); atomicMax(&g_dbg[(base) + 1], d_); atomicAdd(&g_dbg[(base) + 2], 1ull); } } while (0)
 #else
+#define PH_WG_BEGIN do { } while (0)
+#define PH_WG_END(base) do { } while (0)
 #define PH_BEGIN(n) do { } while (0)
 #define PH(i) do { } while (0)
 #define PH_END(base, n) do { } while (0)
@@ -466,6 +473,7 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
     constexpr int TILE_RECS = L1_THREADS * RPT;
     constexpr int TILE_KMERS = L1_THREADS * KPT;
     const uint32_t BLK = 1u << blk_sh;
+    PH_WG_BEGIN;
     constexpr uint64_t DEAD = ~0ull;
     const uint32_t F1 = P.F1;
     const uint32_t F1a = (F1 + 3) & ~3u;
@@ -764,6 +772,7 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
         if (c == 0 || sl < c || bcur[d] == DEAD) continue;
         rec[bcur[d] + sl] = ~0ull;
     }
+    PH_WG_END(40);
 }
 
 // ---------------------------------------------------------------------------

@@ -47,3 +47,6 @@ for it in range(2):
             continue
         print("  %-20s %s" % (name, "  ".join("%s %.1f%%" % (lab, 100.0 * v / tot) for lab, v in zip(labels, vals))),
               flush=True)
+    if dbg[42]:   # scatter_l1f workgroup wall times (100 MHz clock, PH_WG_*)
+        print("  scatter_l1f workgroups %d: mean %.2f ms, max %.2f ms (per launch: all resident at once)"
+              % (dbg[42], dbg[40] / dbg[42] / 1e5, dbg[41] / 1e5), flush=True)
