@@ -42,6 +42,10 @@ struct ApplyArgs {
     int coarse, cjs;
     uint32_t *wco;
     unsigned long long *cw_cur;
+    // dynamic region order (k_apply_count): workgroup w starts with regions
+    // w, w + G and w + 2G (G = gridDim.x) and takes one more per region from
+    // the queue head ctr[CTR_APQ] (numbered from 3G); 0: the static stride
+    int dyn;
 };
 constexpr int MAX_CW = 64;
 
@@ -197,22 +201,50 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
     uint32_t *ccur = (uint32_t *)(cgb + MAX_CW);           // [MAX_CW] placement cursors
     const uint32_t MAXC = KIND == BYTE ? 255u : 15u;
     const bool bigc = KIND == BYTE && P.use_bigcount;
+    PH_WG_BEGIN;
     const uint32_t t = threadIdx.x;
     uint64_t occ = 0;
     const uint64_t total = A.rprefix[P.n];
     Prefetch cur, nxt;
+    // this workgroup's regions: rr, then r1 (prefetched during rr), then r2
+    // (its bounds loaded during rr); the one after r2 is taken during rr
+    // (dynamic order) and published through s_q[parity] after a barrier
+    const uint64_t G = gridDim.x;
+    uint64_t r1 = blockIdx.x + G, r2 = blockIdx.x + 2 * G;
+    uint32_t *s_q = (uint32_t *)(ccur + MAX_CW);   // [2]
+    uint32_t par = 0;
     prefetch_region<KIND, TH>(P, A, blockIdx.x, total, load_bounds(P, A, blockIdx.x, total), cur);
-    Bounds bnext = load_bounds(P, A, blockIdx.x + gridDim.x, total);
+    Bounds bnext = load_bounds(P, A, r1, total);
     PH_BEGIN(8);
-    for (uint64_t rr = blockIdx.x; rr < total; rr += gridDim.x) {
+    for (uint64_t rr = blockIdx.x; rr < total;) {
+        unsigned long long qn = 0;
+        if (A.dyn && t == 0) qn = atomicAdd((unsigned long long *)&A.ctr[CTR_APQ], 1ull);
+        // after a barrier of this region: publish the region after r2, and
+        // move on (the slot of parity par is rewritten two regions later,
+        // after every thread has passed a barrier of the next region)
+        auto publish = [&]() {
+            if (A.dyn && t == 0) s_q[par] = (uint32_t)min<unsigned long long>(qn + 3 * G, total);
+        };
+        auto advance = [&]() {
+            rr = r1;
+            r1 = r2;
+            r2 = A.dyn ? (uint64_t)uniform_u32(s_q[par]) : r2 + G;
+            par ^= 1;
+        };
         const RegionInfo ri = cur.ri;
         if (ri.e0 == ri.e1) {
             if (t == 0) A.wcnt[rr] = 0;
-            prefetch_region<KIND, TH>(P, A, rr + gridDim.x, total, bnext, cur);
-            bnext = load_bounds(P, A, rr + 2 * (uint64_t)gridDim.x, total);
+            prefetch_region<KIND, TH>(P, A, r1, total, bnext, cur);
+            bnext = load_bounds(P, A, r2, total);
+            if (A.dyn) {
+                block_sync();
+                publish();
+                block_sync();
+            }
+            advance();
             continue;
         }
-        const Bounds bafter = load_bounds(P, A, rr + 2 * (uint64_t)gridDim.x, total);
+        const Bounds bafter = load_bounds(P, A, r2, total);
         const uint32_t nb = ri.nb;
         const uint32_t nchunk = (nb + 15) / 16;   // 16 bins per chunk
         uint8_t *tab = A.tab + P.tbyte[ri.i];
@@ -395,12 +427,13 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
                 }
             }
             block_sync();
+            publish();
             PH(2);
             if (bigc && t == 0 && s_flag[1]) {
                 const uint64_t seg = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
                 A.xseg[seg] = make_uint4((uint32_t)ri.e0, (uint32_t)(ri.e0 >> 32), (uint32_t)(ri.e1 - ri.e0), s_flag[1]);
             }
-            prefetch_region<KIND, TH>(P, A, rr + gridDim.x, total, bnext, nxt);
+            prefetch_region<KIND, TH>(P, A, r1, total, bnext, nxt);
             bnext = bafter;
             write_back();
             PH(6);
@@ -445,16 +478,18 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
             block_sync();
             PH(3);
             cur = nxt;
+            advance();
             continue;
         }
         const uint32_t wex = wave_winner_scan(nw, s_wt);
         block_sync();
+        publish();
         PH(2);
         if (bigc && t == 0 && s_flag[1]) {
             const uint64_t seg = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
             A.xseg[seg] = make_uint4((uint32_t)ri.e0, (uint32_t)(ri.e0 >> 32), (uint32_t)(ri.e1 - ri.e0), s_flag[1]);
         }
-        prefetch_region<KIND, TH>(P, A, rr + gridDim.x, total, bnext, nxt);
+        prefetch_region<KIND, TH>(P, A, r1, total, bnext, nxt);
         bnext = bafter;
         write_back();
         uint32_t wall;
@@ -483,7 +518,9 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
         block_sync();
         PH(3);
         cur = nxt;
+        advance();
     }
+    PH_WG_END(43);
     PH_END(16, 8);
     occ = wave_sum(occ);
     if ((threadIdx.x & 63) == 0 && occ) atomicAdd((unsigned long long *)&A.ctr[CTR_OCC], (unsigned long long)occ);

@@ -284,6 +284,17 @@ static uint32_t device_cus(const Graph *g) {
 // records per thread and tile: 8 (3 workgroups per CU; 16 records with 2
 // workgroups per CU measured slower, 117 vs 112 ms/step, round 2)
 static int l1f_rpt() { return L1_MAX_RPT; }
+// tiles per dynamically scheduled k_scatter_l1f chunk (0: one fixed share
+// per workgroup); KH_L1_CHUNK overrides (development)
+static uint32_t l1f_chunk_tiles() {
+    static const int v = env_seg("KH_L1_CHUNK", 32);
+    return (uint32_t)std::max(0, v);
+}
+// dynamic region order in k_apply_count (KH_APPLY_DYN=0: the static stride; development)
+static bool apply_dynamic() {
+    static const bool v = env_seg("KH_APPLY_DYN", 1) != 0;
+    return v;
+}
 // tables per k_scatter_l1f launch (development A/B: fewer tables per launch
 // means fewer live buckets and longer runs per tile, at one k-mer hash per launch)
 static int l1f_tables_per_launch() {
@@ -342,7 +353,7 @@ static OwnL1FFn<Src> own_l1f_kernel(int kpt, bool tw) {
 }
 template <class Src>
 using L1FFn = void (*)(Params, Src, uint64_t, uint64_t, int, int, const uint64_t *, unsigned long long *, uint64_t *,
-                       uint64_t *, int, uint32_t);
+                       uint64_t *, int, uint32_t, uint32_t);
 // fixed-length 2-bit reads whose tiles span at most L1F_TW packed words take
 // the LDS-staged variant (k_scatter_l1f<..., TW = true>)
 template <class Src>
@@ -608,7 +619,7 @@ static size_t lds_apply(const Params &P, bool coarse = false) {
     const size_t R = (size_t)1 << P.s0;
     if (P.kind == BIT)   // coarse-window winners: window arrays + a winner staging array
         return R * 4 + 16 + 64 + R / 8 + (coarse ? MAX_CW * 20 + R * 4 : 0);
-    return R * 4 * 2 + (R / 512) * 4 + 64 + R / 8 + 16 + R + R / 4 + MAX_CW * 20;
+    return R * 4 * 2 + (R / 512) * 4 + 64 + R / 8 + 16 + R + R / 4 + MAX_CW * 20 + 8;   // + s_q[2]
 }
 
 // A shard's level 1 through k_own_filter (kh_partition.cuh) when it owns a
@@ -797,6 +808,7 @@ static void pass_apply(Graph *g, PassState &ps, bool l2f) {
     A.cjs = std::max(q.js, ceil_log2(nkmers) - 6);
     A.wco = win;
     A.cw_cur = nullptr;
+    A.dyn = apply_dynamic() ? 1 : 0;
     if (ps.coarse) {
         ps.ncw = (uint32_t)((nkmers + (1ull << A.cjs) - 1) >> A.cjs);
         ps.fpc = 1u << (A.cjs - q.js);
@@ -822,12 +834,15 @@ static void pass_apply(Graph *g, PassState &ps, bool l2f) {
     else if (P.kind == BIT)
         TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit<APPLY_THREADS>, dim3(agrid), dim3(APPLY_THREADS),
                                               lds_apply(P), st, P, A));
-    else if (P.kind == NIBBLE)
+    else if (P.kind == NIBBLE) {
+        KH_HIP(hipMemsetAsync(w.ctr + CTR_APQ, 0, 8, st));   // the region queue's head
         TIMED("apply_nibble", hipLaunchKernelGGL(apply_count_kernel<NIBBLE>(P), dim3(agrid_count(g, q)),
                                                  dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
-    else
+    } else {
+        KH_HIP(hipMemsetAsync(w.ctr + CTR_APQ, 0, 8, st));   // the region queue's head
         TIMED("apply_byte", hipLaunchKernelGGL(apply_count_kernel<BYTE>(P), dim3(agrid_count(g, q)),
                                                dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
+    }
     if (bigc)
         TIMED("crossing", hipLaunchKernelGGL(k_crossing, dim3(1024), dim3(256), 0, st, P, w.rec2, w.xseg, wout,
                                              w.ctr, w.fullf));
@@ -940,11 +955,12 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                 while (kpt * 2 * nt <= rpt) kpt *= 2;
                 const uint64_t tk = (uint64_t)L1_THREADS * kpt;
                 const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
+                KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, st));   // the chunk queue's head
                 TIMED("scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt, !window && l1f_tw(src, kpt)),
                                                        dim3(nwg), dim3(L1_THREADS),
                                                        lds_scatter_l1f(P, window, (int)tk), st, P, src, nkmers, kpw,
                                                        t0, nt, w.bkt_base, (unsigned long long *)w.bkt_cur, w.rec1,
-                                                       w.ctr, l1f_blk_sh(), 0u));
+                                                       w.ctr, l1f_blk_sh(), 0u, l1f_chunk_tiles()));
             }
         } else if (use_own_filter(g)) {
             nrec = own_filter(g, src, nkmers, window);
@@ -2267,11 +2283,12 @@ static void a2a_level1(Graph *V, const Src &src, uint64_t nkmers, uint32_t jbase
             while (kpt * 2 * nt <= rpt) kpt *= 2;
             const uint64_t tk = (uint64_t)L1_THREADS * kpt;
             const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
+            KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, st));   // the chunk queue's head
             TIMED_G(V, "scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt, l1f_tw(src, kpt)), dim3(nwg),
                                                         dim3(L1_THREADS), lds_scatter_l1f(P, false, (int)tk), st, P,
                                                         src, nkmers, kpw, t0, nt, w.bkt_base,
                                                         (unsigned long long *)w.bkt_cur, w.rec1, w.ctr, l1f_blk_sh(),
-                                                        jbase));
+                                                        jbase, l1f_chunk_tiles()));
         }
         uint64_t err = 0;
         KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));

@@ -142,7 +142,7 @@ struct Workspace {
     uint16_t *q_counts = nullptr;
     uint64_t cap_q = 0, cap_q16 = 0;
 };
-enum { CTR_OCC = 0, CTR_UNIQUE, CTR_NCROSS, CTR_NBC, CTR_ERR, CTR_NFULL, CTR_BCFF, CTR_BCOUT, CTR_N };
+enum { CTR_OCC = 0, CTR_UNIQUE, CTR_NCROSS, CTR_NBC, CTR_ERR, CTR_NFULL, CTR_BCFF, CTR_BCOUT, CTR_L1Q, CTR_APQ, CTR_N };
 constexpr uint64_t BC_EMPTY = ~0ull;   // free map slot; events of hash ~0 count in CTR_BCFF
 
 struct Graph {

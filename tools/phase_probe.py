@@ -50,3 +50,6 @@ for it in range(2):
     if dbg[42]:   # scatter_l1f workgroup wall times (100 MHz clock, PH_WG_*)
         print("  scatter_l1f workgroups %d: mean %.2f ms, max %.2f ms (per launch: all resident at once)"
               % (dbg[42], dbg[40] / dbg[42] / 1e5, dbg[41] / 1e5), flush=True)
+    if dbg[45]:   # k_apply_count workgroup wall times
+        print("  apply workgroups %d: mean %.2f ms, max %.2f ms" % (dbg[45], dbg[43] / dbg[45] / 1e5, dbg[44] / 1e5),
+              flush=True)
