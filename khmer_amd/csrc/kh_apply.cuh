@@ -544,22 +544,43 @@ __global__ void __launch_bounds__(TH, 4) k_apply_bit(Params P, ApplyArgs A) {
     uint32_t *cst0 = chist + MAX_CW;            // [MAX_CW] window's first staging slot
     unsigned long long *cgb = (unsigned long long *)(cst0 + MAX_CW);   // [MAX_CW] window's output base
     uint32_t *ccur = (uint32_t *)(cgb + MAX_CW);           // [MAX_CW] placement cursors
-    uint32_t *wst = ccur + MAX_CW;                          // [R] winners in window order (coarse only)
+    uint32_t *s_q = ccur + MAX_CW;                          // [2] dynamic region order (as k_apply_count)
+    uint32_t *wst = s_q + 2;                                // [R] winners in window order (coarse only)
     const uint32_t t = threadIdx.x;
     uint64_t occ = 0;
     const uint64_t total = A.rprefix[P.n];
     Prefetch cur, nxt;
+    const uint64_t G = gridDim.x;   // region order as in k_apply_count
+    uint64_t r1 = blockIdx.x + G, r2 = blockIdx.x + 2 * G;
+    uint32_t par = 0;
     prefetch_region<BIT, TH>(P, A, blockIdx.x, total, load_bounds(P, A, blockIdx.x, total), cur);
-    Bounds bnext = load_bounds(P, A, blockIdx.x + gridDim.x, total);
-    for (uint64_t rr = blockIdx.x; rr < total; rr += gridDim.x) {
+    Bounds bnext = load_bounds(P, A, r1, total);
+    for (uint64_t rr = blockIdx.x; rr < total;) {
+        unsigned long long qn = 0;
+        if (A.dyn && t == 0) qn = atomicAdd((unsigned long long *)&A.ctr[CTR_APQ], 1ull);
+        auto publish = [&]() {
+            if (A.dyn && t == 0) s_q[par] = (uint32_t)min<unsigned long long>(qn + 3 * G, total);
+        };
+        auto advance = [&]() {
+            rr = r1;
+            r1 = r2;
+            r2 = A.dyn ? (uint64_t)uniform_u32(s_q[par]) : r2 + G;
+            par ^= 1;
+        };
         const RegionInfo ri = cur.ri;
         if (ri.e0 == ri.e1) {
             if (t == 0) A.wcnt[rr] = 0;
-            prefetch_region<BIT, TH>(P, A, rr + gridDim.x, total, bnext, cur);
-            bnext = load_bounds(P, A, rr + 2 * (uint64_t)gridDim.x, total);
+            prefetch_region<BIT, TH>(P, A, r1, total, bnext, cur);
+            bnext = load_bounds(P, A, r2, total);
+            if (A.dyn) {
+                block_sync();
+                publish();
+                block_sync();
+            }
+            advance();
             continue;
         }
-        const Bounds bafter = load_bounds(P, A, rr + 2 * (uint64_t)gridDim.x, total);
+        const Bounds bafter = load_bounds(P, A, r2, total);
         const uint32_t nb = ri.nb;
         const uint32_t nchunk = (nb + 127) / 128;   // 16 bytes = 128 bins per chunk
         uint8_t *tab = A.tab + P.tbyte[ri.i] + (ri.bin_lo >> 3);
@@ -586,7 +607,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_bit(Params P, ApplyArgs A) {
             }
         }
         block_sync();
-        prefetch_region<BIT, TH>(P, A, rr + gridDim.x, total, bnext, nxt);
+        prefetch_region<BIT, TH>(P, A, r1, total, bnext, nxt);
         bnext = bafter;
         // pass 1 (thread per bin): winners set their bit (and, coarse, count
         // per window)
@@ -619,6 +640,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_bit(Params P, ApplyArgs A) {
         }
         const uint32_t wex = wave_winner_scan(nw, s_wt);
         block_sync();
+        publish();
         // pass 2: write back changed 128-bin chunks; winners
         for (uint32_t x = t; x < nchunk; x += blockDim.x)
             if ((chg[x >> 5] >> (x & 31)) & 1) ((uint4 *)tab)[x] = ((const uint4 *)bits)[x];
@@ -665,6 +687,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_bit(Params P, ApplyArgs A) {
         }
         block_sync();
         cur = nxt;
+        advance();
     }
     occ = wave_sum(occ);
     if ((threadIdx.x & 63) == 0 && occ) atomicAdd((unsigned long long *)&A.ctr[CTR_OCC], (unsigned long long)occ);

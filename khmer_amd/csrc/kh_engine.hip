@@ -618,7 +618,7 @@ static unsigned agrid_count(const Graph *g, const PassGeo &q) {
 static size_t lds_apply(const Params &P, bool coarse = false) {
     const size_t R = (size_t)1 << P.s0;
     if (P.kind == BIT)   // coarse-window winners: window arrays + a winner staging array
-        return R * 4 + 16 + 64 + R / 8 + (coarse ? MAX_CW * 20 + R * 4 : 0);
+        return R * 4 + 16 + 64 + R / 8 + MAX_CW * 20 + 8 + (coarse ? R * 4 : 0);
     return R * 4 * 2 + (R / 512) * 4 + 64 + R / 8 + 16 + R + R / 4 + MAX_CW * 20 + 8;   // + s_q[2]
 }
 
@@ -828,6 +828,7 @@ static void pass_apply(Graph *g, PassState &ps, bool l2f) {
         A.cw_cur = w.cw_cur;
     }
     const unsigned agrid = (unsigned)std::min<uint64_t>(q.regions, 256 * 2);
+    KH_HIP(hipMemsetAsync(w.ctr + CTR_APQ, 0, 8, st));   // the region queue's head (k_apply_*)
     if (P.kind == BIT && ps.coarse)   // one 1024-thread workgroup per CU (the staging array), else two of 512
         TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit<1024>, dim3((unsigned)std::min<uint64_t>(q.regions, device_cus(g))),
                                               dim3(1024), lds_apply(P, true), st, P, A));
@@ -835,11 +836,9 @@ static void pass_apply(Graph *g, PassState &ps, bool l2f) {
         TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit<APPLY_THREADS>, dim3(agrid), dim3(APPLY_THREADS),
                                               lds_apply(P), st, P, A));
     else if (P.kind == NIBBLE) {
-        KH_HIP(hipMemsetAsync(w.ctr + CTR_APQ, 0, 8, st));   // the region queue's head
         TIMED("apply_nibble", hipLaunchKernelGGL(apply_count_kernel<NIBBLE>(P), dim3(agrid_count(g, q)),
                                                  dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
     } else {
-        KH_HIP(hipMemsetAsync(w.ctr + CTR_APQ, 0, 8, st));   // the region queue's head
         TIMED("apply_byte", hipLaunchKernelGGL(apply_count_kernel<BYTE>(P), dim3(agrid_count(g, q)),
                                                dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
     }

@@ -1414,12 +1414,16 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
         // the list of regions whose pending tail segment completes in this
         // tile (every pending one on the last tile); F2 <= THREADS: thread d
         // owns region d
+        // The reservations' results are stored to nbase only after the tail
+        // flush below (nothing before the stores reads nbase), so their
+        // latency overlaps the flush instead of stalling every wave here.
+        uint64_t nb = 0, nlim = ~0ull;
+        uint32_t nneed = 0;
         {
             const uint32_t d = threadIdx.x;
             bool fl = false;
             if (d < F2) {
                 const uint32_t h = hist[d], c0 = cnt[d];
-                uint64_t nb = 0;
                 const bool dead = bcur[d] == L2F_DEAD;
                 if (h) {
                     const uint32_t need = ((c0 + h + BLK - 1) >> blk_sh) - ((c0 + BLK - 1) >> blk_sh);
@@ -1427,13 +1431,17 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
                         nb = L2F_DEAD;
                     } else if (need) {
                         nb = atomicAdd(&reg_cur[gb + d], (unsigned long long)need * BLK);
-                        if (nb + (uint64_t)need * BLK > reg_base[gb + d + 1]) {
-                            atomicOr((unsigned long long *)&ctr[CTR_ERR], 4ull);
-                            nb = L2F_DEAD;
-                        }
+                        nlim = reg_base[gb + d + 1];
+                        nneed = need;
                     }
                 }
+#ifdef KH_L2_EARLY_NBASE
+                if (nneed && nb + (uint64_t)nneed * BLK > nlim) {
+                    atomicOr((unsigned long long *)&ctr[CTR_ERR], 4ull);
+                    nb = L2F_DEAD;
+                }
                 nbase[d] = nb;
+#endif
                 const uint32_t a = c0 & ~(SEG - 1), e = c0 + h;
                 fl = !dead && c0 != a && (last ? e : (e & ~(SEG - 1))) > a;
             }
@@ -1458,6 +1466,15 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
                 if (a + sl < c0) rec_out[bcur[d] + ((a + sl) & (BLK - 1))] = tail[d * SEG + sl];
             }
         }
+#ifndef KH_L2_EARLY_NBASE
+        if (threadIdx.x < F2) {
+            if (nneed && nb + (uint64_t)nneed * BLK > nlim) {
+                atomicOr((unsigned long long *)&ctr[CTR_ERR], 4ull);
+                nb = L2F_DEAD;
+            }
+            nbase[threadIdx.x] = nb;
+        }
+#endif
         PH(4);
         block_sync();   // the flushed tail slots are refilled below
         PH(5);
