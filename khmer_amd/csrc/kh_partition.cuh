@@ -753,16 +753,15 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             const uint32_t nslot = lstart[dlast] + (hist[dlast] ? (hist[dlast] + (cnt[dlast] & 1u) + 1u) & ~1u : 0u);
             const uint2 *sbj2 = (const uint2 *)sbj;
             const uint2 *stage2 = (const uint2 *)stage;
-            for (uint32_t m = threadIdx.x; 2 * m < nslot; m += L1_THREADS) {
+            const ulonglong2 *dl2 = (const ulonglong2 *)dl;   // both placement constants in one 16-B read
+            auto put_pair = [&](uint32_t m, uint2 bj, uint2 st, uint2 ql, ulonglong2 dd) {
                 const uint32_t q = 2 * m;
-                const uint2 bj = sbj2[m], st = stage2[m];
                 const uint32_t d = bj.x >> 16;
                 const bool r0 = (bj.x & 0xFFFFu) != SLOT_EMPTY, r1 = (bj.y & 0xFFFFu) != SLOT_EMPTY;
                 const uint64_t v0 = ((jbase + j0 + (bj.x & 0xFFFFu)) << 32) | st.x;
                 const uint64_t v1 = ((jbase + j0 + (bj.y & 0xFFFFu)) << 32) | st.y;
-                const uint2 ql = qq[d];   // (qs, qlim): both even
-                if (P.ablate & 16) continue;   // timing only: no run writes
-                const uint64_t o = dl[2 * d + (q >= ql.x ? 1 : 0)] + q;
+                if (P.ablate & 16) return;   // timing only: no run writes
+                const uint64_t o = (q >= ql.x ? dd.y : dd.x) + q;   // (qs, qlim): both even
                 if (q < ql.y) {
                     if (r0 && r1) *(ulonglong2 *)(rec + o) = make_ulonglong2(v0, v1);
                     else if (r0) rec[o] = v0;
@@ -770,7 +769,36 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
                 } else if (r0) {
                     tail[d] = v0;   // the run's unpaired last record
                 }
+            };
+#ifdef KH_L1_WO_BATCH
+            // development: WU pairs per thread per step, their LDS reads issued together
+            constexpr int WU = KH_L1_WO_BATCH;
+            for (uint32_t m0 = threadIdx.x; 2 * m0 < nslot; m0 += WU * L1_THREADS) {
+                uint2 bj[WU], st[WU], ql[WU];
+                ulonglong2 dd[WU];
+#pragma unroll
+                for (int u = 0; u < WU; u++) {
+                    const uint32_t m = m0 + (uint32_t)u * L1_THREADS;
+                    const bool ok = 2 * m < nslot;
+                    bj[u] = ok ? sbj2[m] : make_uint2(SLOT_EMPTY, SLOT_EMPTY);
+                    st[u] = ok ? stage2[m] : make_uint2(0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < WU; u++) {
+                    const uint32_t d = bj[u].x >> 16;
+                    ql[u] = qq[d];
+                    dd[u] = dl2[d];
+                }
+#pragma unroll
+                for (int u = 0; u < WU; u++) put_pair(m0 + (uint32_t)u * L1_THREADS, bj[u], st[u], ql[u], dd[u]);
             }
+#else
+            for (uint32_t m = threadIdx.x; 2 * m < nslot; m += L1_THREADS) {
+                const uint2 bj = sbj2[m];
+                const uint32_t d = bj.x >> 16;
+                put_pair(m, bj, stage2[m], qq[d], dl2[d]);
+            }
+#endif
         }
         PH(6);
         block_sync();
