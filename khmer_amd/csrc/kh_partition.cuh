@@ -1442,9 +1442,10 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
         // the list of regions whose pending tail segment completes in this
         // tile (every pending one on the last tile); F2 <= THREADS: thread d
         // owns region d
-        // The reservations' results are stored to nbase only after the tail
-        // flush below (nothing before the stores reads nbase), so their
-        // latency overlaps the flush instead of stalling every wave here.
+        // The reservations' results go to nbase here.  (-DKH_L2_LATE_NBASE
+        // stores them only after the tail flush, to overlap the atomics'
+        // latency with it: measured slower, 93.7-95.0 vs 90.2 ms/step, since
+        // waiting for the atomic then also waits for the flush stores.)
         uint64_t nb = 0, nlim = ~0ull;
         uint32_t nneed = 0;
         {
@@ -1463,7 +1464,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
                         nneed = need;
                     }
                 }
-#ifdef KH_L2_EARLY_NBASE
+#ifndef KH_L2_LATE_NBASE
                 if (nneed && nb + (uint64_t)nneed * BLK > nlim) {
                     atomicOr((unsigned long long *)&ctr[CTR_ERR], 4ull);
                     nb = L2F_DEAD;
@@ -1494,7 +1495,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
                 if (a + sl < c0) rec_out[bcur[d] + ((a + sl) & (BLK - 1))] = tail[d * SEG + sl];
             }
         }
-#ifndef KH_L2_EARLY_NBASE
+#ifdef KH_L2_LATE_NBASE
         if (threadIdx.x < F2) {
             if (nneed && nb + (uint64_t)nneed * BLK > nlim) {
                 atomicOr((unsigned long long *)&ctr[CTR_ERR], 4ull);
