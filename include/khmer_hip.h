@@ -233,6 +233,12 @@ int kh_device_synchronize(int device);
 /* per-kernel HIP-event timing on the graph's stream: on=1 resets and enables;
  * stats are text lines "kernel<TAB>launches<TAB>total_ms" */
 int kh_graph_set_profiling(kh_graph *g, int on);
+/* work distribution of the fixed-capacity level 1 and of apply (no reference
+ * counterpart; results are identical either way): l1_chunk_tiles = tiles per
+ * dynamically scheduled level-1 chunk (0: one fixed share per workgroup),
+ * apply_dynamic = 1 regions from a queue / 0 fixed stride; -1 keeps the
+ * default (KH_L1_CHUNK / KH_APPLY_DYN, else 32 and 1) */
+int kh_graph_set_schedule(kh_graph *g, int l1_chunk_tiles, int apply_dynamic);
 int kh_graph_kernel_stats(kh_graph *g, char *buf, size_t cap, size_t *len);
 
 /* ---------------- multi-GPU sharded groups ----------------------------------

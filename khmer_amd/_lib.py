@@ -107,6 +107,7 @@ SIGNATURES = {
     "kh_device_free": (i32, [i32, P]),
     "kh_device_synchronize": (i32, [i32]),
     "kh_graph_set_profiling": (i32, [P, i32]),
+    "kh_graph_set_schedule": (i32, [P, i32, i32]),
     "kh_graph_kernel_stats": (i32, [P, ctypes.c_char_p, sz, PSZ]),
 }
 

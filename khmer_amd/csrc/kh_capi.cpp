@@ -1317,6 +1317,16 @@ extern "C" int kh_graph_set_profiling(kh_graph *h, int on) {
     });
 }
 
+extern "C" int kh_graph_set_schedule(kh_graph *h, int l1_chunk_tiles, int apply_dynamic) {
+    return guard([&] {
+        CHECK_PTR(h);
+        Graph *g = h->g;
+        std::lock_guard<std::recursive_mutex> lk(g->mu);
+        g->l1_chunk = l1_chunk_tiles < 0 ? -1 : l1_chunk_tiles;
+        g->apply_dyn = apply_dynamic < 0 ? -1 : (apply_dynamic != 0);
+    });
+}
+
 extern "C" int kh_graph_kernel_stats(kh_graph *h, char *buf, size_t cap, size_t *len) {
     return guard([&] {
         CHECK_PTR(h);

@@ -286,14 +286,14 @@ static uint32_t device_cus(const Graph *g) {
 static int l1f_rpt() { return L1_MAX_RPT; }
 // tiles per dynamically scheduled k_scatter_l1f chunk (0: one fixed share
 // per workgroup); KH_L1_CHUNK overrides (development)
-static uint32_t l1f_chunk_tiles() {
+static uint32_t l1f_chunk_tiles(const Graph *g) {
     static const int v = env_seg("KH_L1_CHUNK", 32);
-    return (uint32_t)std::max(0, v);
+    return (uint32_t)std::max(0, g->l1_chunk >= 0 ? g->l1_chunk : v);
 }
 // dynamic region order in k_apply_count (KH_APPLY_DYN=0: the static stride; development)
-static bool apply_dynamic() {
+static bool apply_dynamic(const Graph *g) {
     static const bool v = env_seg("KH_APPLY_DYN", 1) != 0;
-    return v;
+    return g->apply_dyn >= 0 ? g->apply_dyn != 0 : v;
 }
 // tables per k_scatter_l1f launch (development A/B: fewer tables per launch
 // means fewer live buckets and longer runs per tile, at one k-mer hash per launch)
@@ -808,7 +808,7 @@ static void pass_apply(Graph *g, PassState &ps, bool l2f) {
     A.cjs = std::max(q.js, ceil_log2(nkmers) - 6);
     A.wco = win;
     A.cw_cur = nullptr;
-    A.dyn = apply_dynamic() ? 1 : 0;
+    A.dyn = apply_dynamic(g) ? 1 : 0;
     if (ps.coarse) {
         ps.ncw = (uint32_t)((nkmers + (1ull << A.cjs) - 1) >> A.cjs);
         ps.fpc = 1u << (A.cjs - q.js);
@@ -959,7 +959,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                                                        dim3(nwg), dim3(L1_THREADS),
                                                        lds_scatter_l1f(P, window, (int)tk), st, P, src, nkmers, kpw,
                                                        t0, nt, w.bkt_base, (unsigned long long *)w.bkt_cur, w.rec1,
-                                                       w.ctr, l1f_blk_sh(), 0u, l1f_chunk_tiles()));
+                                                       w.ctr, l1f_blk_sh(), 0u, l1f_chunk_tiles(g)));
             }
         } else if (use_own_filter(g)) {
             nrec = own_filter(g, src, nkmers, window);
@@ -2287,7 +2287,7 @@ static void a2a_level1(Graph *V, const Src &src, uint64_t nkmers, uint32_t jbase
                                                         dim3(L1_THREADS), lds_scatter_l1f(P, false, (int)tk), st, P,
                                                         src, nkmers, kpw, t0, nt, w.bkt_base,
                                                         (unsigned long long *)w.bkt_cur, w.rec1, w.ctr, l1f_blk_sh(),
-                                                        jbase, l1f_chunk_tiles()));
+                                                        jbase, l1f_chunk_tiles(V)));
         }
         uint64_t err = 0;
         KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));

@@ -152,6 +152,7 @@ struct Graph {
     // table (lo = 0, lsz = sizes when not sharded); nbytes are the slice's bytes
     int world = 1, rank = 0;
     bool grouped = false;             // a shard of a ShardGroup (its winners are routed by window)
+    int l1_chunk = -1, apply_dyn = -1;   // work distribution (kh_graph_set_schedule; -1: default)
     int force_s2 = -1;                // level-2 fan-out fixed by the group (exchange mode: the
                                       // unsharded geometry's, so level-1 buckets line up)
     std::vector<uint64_t> lo, lsz;
