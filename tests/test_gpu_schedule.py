@@ -73,7 +73,15 @@ def test_schedule_matches_oracle(stream, l1_chunk, apply_dyn):
     g.set_use_bigcount(True)
     check(lib.kh_graph_set_schedule(g._g, l1_chunk, apply_dyn))
     check(lib.kh_graph_set_batch_kmers(g._g, 150000))   # six device passes
+    check(lib.kh_graph_set_profiling(g._g, 1))
     check(lib.kh_consume_packed_fixed_device(g._g, stream["words"], stream["n"], stream["L"]))
+    # the fixed-capacity level 1 and level 2 ran (no histogram pass): the
+    # schedule under test was the one used
+    buf = ctypes.create_string_buffer(1 << 16)
+    n = ctypes.c_size_t()
+    check(lib.kh_graph_kernel_stats(g._g, buf, len(buf), ctypes.byref(n)))
+    kernels = {ln.split("\t")[0] for ln in buf.value.decode().splitlines() if ln}
+    assert {"scatter_l1", "scatter_l2", "apply_byte"} <= kernels and not kernels & {"hist_l1", "hist_l2"}, kernels
     want = stream["want"]
     tabs = g.get_raw_tables()
     for i in range(4):
