@@ -331,7 +331,7 @@ static size_t lds_own_l1f(const Params &P) {
 static bool own_l1f_on() { static const bool v = env_seg("KH_OWN_L1F", 1) != 0; return v; }
 template <class Src>
 using OwnL1FFn = void (*)(Params, Src, uint64_t, uint64_t, int, int, const uint64_t *, unsigned long long *,
-                          uint64_t *, uint64_t *, int);
+                          uint64_t *, uint64_t *, int, uint32_t);
 template <class Src>
 static OwnL1FFn<Src> own_l1f_kernel(int kpt, bool tw) {
     if constexpr (std::is_same<Src, SrcTwoBit>::value) {
@@ -936,9 +936,11 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                 while (kpt * 2 * nt <= 8) kpt *= 2;
                 const uint64_t tk = (uint64_t)L1_THREADS * kpt;
                 const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
+                KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, st));   // the chunk queue's head
                 TIMED("own_l1f", hipLaunchKernelGGL(own_l1f_kernel<Src>(kpt, l1f_tw(src, kpt)), dim3(nwg), dim3(L1_THREADS),
                                                     lds_own_l1f(P), st, P, src, nkmers, kpw, t0, nt, w.bkt_base,
-                                                    (unsigned long long *)w.bkt_cur, w.rec1, w.ctr, l1f_blk_sh()));
+                                                    (unsigned long long *)w.bkt_cur, w.rec1, w.ctr, l1f_blk_sh(),
+                                                    l1f_chunk_tiles(g)));
             }
         } else if (l1f) {
             ensure_recs(g, std::max(cap1, cap2));

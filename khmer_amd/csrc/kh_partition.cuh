@@ -968,7 +968,7 @@ constexpr int OWNF_BUF = OWN_BATCH + L1_THREADS * OWN_FSLOTS;  // < OWN_BATCH le
 template <class Src, int KPT, bool TW_ = false>
 __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint64_t nkmers, uint64_t kpw, int t0,
                                                        int nt, const uint64_t *bkt_base, unsigned long long *bkt_cur,
-                                                       uint64_t *rec, uint64_t *ctr, int blk_sh) {
+                                                       uint64_t *rec, uint64_t *ctr, int blk_sh, uint32_t cht) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int RPT = OWN_BATCH / L1_THREADS;
     constexpr int FSLOTS = OWN_FSLOTS;
@@ -1000,15 +1000,22 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
         cnt[b] = 0;
         hist[b] = 0;
     }
-    const uint64_t c0 = min(nkmers, (uint64_t)blockIdx.x * kpw);
-    const uint64_t c1 = min(nkmers, c0 + kpw);
+    // chunks of CK k-mers: a fixed share per workgroup (cht == 0) or chunks of
+    // cht tiles from the queue head ctr[CTR_L1Q], as in k_scatter_l1f
+    const uint64_t CK = cht ? (uint64_t)cht * TILE_KMERS : kpw;
+    const uint32_t nchunks = (uint32_t)((nkmers + CK - 1) / CK);
+    uint32_t cb = cht ? blockIdx.x + gridDim.x : nchunks;
+    uint64_t j0 = min(nkmers, (uint64_t)blockIdx.x * CK);
+    uint64_t ce = min(nkmers, j0 + CK);
+    bool chunk_top = true;
+    uint32_t *s_q = s_wtot + 47;   // the batch scan uses s_wtot[32, 40)
     constexpr int NPEND = TW ? 1 : KPT;
     typename Src::Pend pend[NPEND];
     if (!TW) {
 #pragma unroll
         for (int a = 0; a < NPEND; a++) {
-            const uint64_t j = c0 + (uint64_t)a * L1_THREADS + threadIdx.x;
-            if (j < min(c1, c0 + TILE_KMERS)) pend[a] = kmer_fetch(src, j);
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            if (j < min(ce, j0 + TILE_KMERS)) pend[a] = kmer_fetch(src, j);
         }
     }
     auto tile_w0 = [&](uint64_t j0) -> uint64_t {
@@ -1018,9 +1025,9 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
     auto tile_nw = [&](uint64_t j0, uint64_t j1) -> uint32_t { return (uint32_t)(tile_w0(j1 - 1) + 2 - tile_w0(j0)); };
     uint64_t tw_next = 0;
     if constexpr (TW) {
-        if (c1 > c0) {
-            const uint64_t e = min(c1, c0 + TILE_KMERS);
-            if (threadIdx.x < tile_nw(c0, e)) s_tw[threadIdx.x] = src.words[tile_w0(c0) + threadIdx.x];
+        if (ce > j0) {
+            const uint64_t e = min(ce, j0 + TILE_KMERS);
+            if (threadIdx.x < tile_nw(j0, e)) s_tw[threadIdx.x] = src.words[tile_w0(j0) + threadIdx.x];
         }
         block_sync();
     }
@@ -1109,10 +1116,19 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
 
     uint32_t nbuf = 0;   // records in buf (block-uniform)
     bool flushed_last = false;
-    const uint32_t ntiles = uniform_u32((uint32_t)((c1 - c0 + TILE_KMERS - 1) / TILE_KMERS));
-    for (uint32_t ti = 0; ti < ntiles; ti++) {
-        const uint64_t j0 = c0 + (uint64_t)ti * TILE_KMERS;
-        const uint64_t j1 = min(c1, j0 + TILE_KMERS);
+    for (uint32_t ti = 0; j0 < ce; ti++) {
+        const uint64_t j1 = min(ce, j0 + TILE_KMERS);
+        // the next tile [n0, n1): in this chunk, else the first of chunk cb
+        uint64_t n0 = j1, n1 = j1;
+        if (j1 < ce) {
+            n1 = min(ce, j1 + TILE_KMERS);
+        } else if (cb < nchunks) {
+            n0 = (uint64_t)cb * CK;
+            n1 = min(nkmers, n0 + min(CK, (uint64_t)TILE_KMERS));
+        }
+        const bool more = n1 > n0;   // a next tile exists
+        unsigned long long qn = 0;
+        if (cht && chunk_top && threadIdx.x == 0) qn = atomicAdd((unsigned long long *)&ctr[CTR_L1Q], 1ull);
         uint64_t v[FSLOTS];
         uint32_t own = 0;   // bit q: record slot q is owned here
         uint64_t hh[KPT];
@@ -1131,8 +1147,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
                 }
                 hh[a] = h;
             }
-            if (ti + 1 < ntiles) {   // the next tile's words (stored after this tile's scan barrier)
-                const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
+            if (more) {   // the next tile's words (stored after this tile's scan barrier)
                 if (threadIdx.x < tile_nw(n0, n1)) tw_next = src.words[tile_w0(n0) + threadIdx.x];
             }
         } else {
@@ -1141,7 +1156,6 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
                 const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
                 hh[a] = j < j1 ? src.finish(pend[a]) : 0;
             }
-            const uint64_t n0 = j0 + TILE_KMERS, n1 = min(c1, n0 + TILE_KMERS);
 #pragma unroll
             for (int a = 0; a < NPEND; a++) {
                 const uint64_t j = n0 + (uint64_t)a * L1_THREADS + threadIdx.x;
@@ -1184,9 +1198,12 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
         nbuf += tot;
         if (P.ablate & 64) nbuf = 0;   // timing only: the filter without the bucket placement
         // buffer (ti + 1) & 1 was last read in tile ti - 1, before this tile's scan barrier
-        if (TW && ti + 1 < ntiles && threadIdx.x < L1F_TW) s_tw[((ti + 1) & 1) * L1F_TW + threadIdx.x] = tw_next;
+        if (TW && more && threadIdx.x < L1F_TW) s_tw[((ti + 1) & 1) * L1F_TW + threadIdx.x] = tw_next;
+        // the chunk taken from the queue (after this tile's first barrier:
+        // every thread has read the previous value), read after the next one
+        if (cht && chunk_top && threadIdx.x == 0) *s_q = (uint32_t)min<unsigned long long>(qn + 2ull * gridDim.x, nchunks);
         block_sync();
-        const bool lt = ti + 1 == ntiles;
+        const bool lt = !more;
         uint32_t o = 0;   // batches buf[o, o + OWN_BATCH) in order; the rest (< OWN_BATCH) moves to the front
         while (nbuf - o >= (uint32_t)OWN_BATCH || (lt && !flushed_last)) {
             const uint32_t n = min(nbuf - o, (uint32_t)OWN_BATCH);
@@ -1199,6 +1216,15 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
             for (uint32_t x = threadIdx.x; x < nbuf - o; x += blockDim.x) buf[x] = buf[o + x];
             nbuf -= o;
             block_sync();
+        }
+        // advance: the next tile of this chunk, or the first of chunk cb
+        chunk_top = j1 >= ce;
+        if (chunk_top) {
+            j0 = n0;
+            ce = cb < nchunks ? min(nkmers, (uint64_t)cb * CK + CK) : n0;
+            cb = cht ? uniform_u32(*s_q) : nchunks;
+        } else {
+            j0 = j1;
         }
     }
     block_sync();
