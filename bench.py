@@ -89,7 +89,8 @@ def parse():
     ap.add_argument("--query", action="store_true",
                     help="time get_median_count over the reads (tables built from them first, untimed)")
     ap.add_argument("--ablate", type=int, default=0,
-                    help="timing-only KH_ABLATE bits (results become wrong; never for reported numbers)")
+                    help="timing-only KH_ABLATE bits (results become wrong; never for reported numbers); "
+                         "needs a development library built with make EXTRA_HIPFLAGS=-DKH_ABLATE")
     ap.add_argument("--variable-path", action="store_true",
                     help="feed k-mer offsets (variable-length read path) instead of the fixed-length path")
     ap.add_argument("--cpu-reads", type=int, default=1_000_000,
@@ -111,12 +112,17 @@ def parse():
 FIXTURE_GRAPH = {(1, 0): "Countgraph", (2, 0): "Nodegraph", (7, 0): "SmallCountgraph", (7, 1): "SmallCounttable"}
 
 
-def matching_fixture(args, total_reads):
+def matching_fixture(args, total_reads, exchange=None):
     """The oracle golden fixture (tests/golden/full/*.json, made by
     tests/golden/make_full_fixtures.py) whose workload is exactly this run's
     whole stream, if any: then the bench line carries a parity check of its
-    own (counters and per-table SHA-256 against the single-threaded oracle)."""
+    own (counters and per-table SHA-256 against the single-threaded oracle).
+    exchange = [world, batch_kmers] for an exchange-mode group, whose stream
+    is pass-interleaved: a fixture made in that order matches exactly; failing
+    that, the rank-order fixture of the same reads (order-free outputs only).
+    Returns (fixture, exact_order)."""
     import glob
+    same_reads, interleaved = None, None
     for path in sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "full", "*.json"))):
         try:
             with open(path) as fh:
@@ -127,17 +133,27 @@ def matching_fixture(args, total_reads):
         if (FIXTURE_GRAPH.get((p["kind"], p["hash"])) == args.graph and p["k"] == args.k and p["n"] == args.tables
                 and float(p["x"]) == float(args.x) and p["reads"] == total_reads and p["L"] == args.read_len
                 and bool(p["bigcount"]) == bool(args.bigcount) and int(p["genome"]) == int(args.genome)):
-            return fx
-    return None
+            order = p.get("exchange")
+            if order is None and same_reads is None:
+                same_reads = fx
+            elif exchange is not None and order == list(exchange):
+                interleaved = fx
+    if exchange is None:
+        return (same_reads, True) if same_reads is not None else (None, False)
+    if interleaved is not None:
+        return interleaved, True
+    return (same_reads, False) if same_reads is not None else (None, False)
 
 
 def compare_fixture(fx, n_unique, n_occupied, table_sha, stream_order=True):
-    """stream_order=False (exchange mode: a pass-interleaved stream): the
-    tables and n_occupied do not depend on the order; n_unique does, so it is
-    not compared."""
+    """stream_order=False (an exchange-mode run with no fixture in its
+    pass-interleaved order): the tables and n_occupied do not depend on the
+    order and are compared; n_unique does and is reported beside the
+    rank-order fixture's."""
     if not stream_order:
         out = {"fixture": fx["config"], "n_occupied_match": n_occupied == fx["n_occupied"],
-               "n_unique": "pass-interleaved stream (not the fixture's order): not compared"}
+               "n_unique": "pass-interleaved stream: no fixture in this order (rank-order fixture %d, run %d)"
+                           % (fx["n_unique_kmers"], n_unique)}
         if table_sha is not None:
             out["tables_match"] = list(table_sha) == list(fx["table_sha256"])
         return out
@@ -377,12 +393,19 @@ def main():
         unprof = runner.max_over_ranks(u1 - u0) * 1e3 / args.steps
     check_info = runner.check()
     # parity of the timed workload itself, when a golden fixture holds it
-    fx = None if args.query else matching_fixture(args, nreads * world)
+    fx, exact_order = matching_fixture(args, nreads * world,
+                                       [world, args.batch_kmers] if (args.exchange and world > 1) else None)
+    if args.query:
+        # the tables were built untimed from the same reads; the fixture's
+        # get_median_count digest (median, average, stddev of its first reads)
+        if fx is not None and fx.get("median_sha256") and rank == 0:
+            check_info.update(runner.query_check(fx))
+        fx = None
     if fx is not None:
         sha = runner.table_sha256()   # collective when sharded
         if rank == 0:
             check_info.update(compare_fixture(fx, check_info["n_unique_kmers"], check_info["n_occupied"], sha,
-                                              stream_order=not (args.exchange and world > 1)))
+                                              stream_order=exact_order))
 
     bpk = query_bytes_per_kmer(L, k, nt) if args.query else algorithmic_bytes_per_kmer(L, k, nt)
     total_kmers = nkmers * world * args.steps
@@ -560,13 +583,33 @@ class SingleGpuBench(object):
         out = {"n_unique_kmers": self.g.n_unique_kmers(), "n_occupied": self.g.n_occupied()}
 
         if self.args.query:
-            import hashlib
-            n = self.args.reads
-            med = (ctypes.c_uint16 * n)()
-            self._ck(self.lib.kh_device_synchronize(self.device))
-            hip_copy_d2h(self.lib, self.device, med, self.med, n * 2)
-            out["median_sha256"] = hashlib.sha256(bytes(med)).hexdigest()
+            from tests import full_digest as FD
+            med, avg, sd = self.query_outputs()
+            out["median_sha256"] = FD.median_digest(med, avg, sd)   # medians, averages and stddevs
+            out["median_max"] = int(med.max()) if len(med) else 0
         return out
+
+    def query_outputs(self):
+        """(median u16, average f32, stddev f32) numpy arrays of the last query."""
+        import numpy as np
+        n = self.args.reads
+        med = np.zeros(n, np.uint16)
+        avg = np.zeros(n, np.float32)
+        sd = np.zeros(n, np.float32)
+        self._ck(self.lib.kh_device_synchronize(self.device))
+        for arr, dev in ((med, self.med), (avg, self.avg), (sd, self.sd)):
+            hip_copy_d2h(self.lib, self.device, arr.ctypes.data_as(ctypes.c_void_p), dev, arr.nbytes)
+        return med, avg, sd
+
+    def query_check(self, fx):
+        """The fixture's get_median_count digest over its first median_reads
+        reads (tests/golden/make_full_fixtures.py: the oracle's float32
+        results, bit patterns exactly)."""
+        from tests import full_digest as FD
+        n = fx["median_reads"]
+        med, avg, sd = self.query_outputs()
+        return {"fixture": fx["config"], "median_reads": n,
+                "median_match": FD.median_digest(med[:n], avg[:n], sd[:n]) == fx["median_sha256"]}
 
     def close(self):
         for p in self.bufs:

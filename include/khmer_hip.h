@@ -307,6 +307,26 @@ int kh_group_mode(kh_group *grp, int *mode);
 /* bins [lo, lo + size) of table `table` held by rank `rank` (any rank) */
 int kh_group_rank_slice(kh_group *grp, int rank, int table, uint64_t *lo, uint64_t *size);
 int kh_group_counters(kh_group *grp, uint64_t *n_unique, uint64_t *n_occupied);   /* collective */
+/* The Counttable family (MurmurHash3) in a group: the same
+ * collective consume over ASCII fixed-length reads (d_bytes[l] = local shard
+ * l's own reads; hash_kind KH_HASH_MURMUR at group creation).  Replaces the
+ * per-rank consume loop (src/oxli/hashtable.cc:106-133) of
+ * MurmurHashtable / SmallCounttable (include/oxli/hashtable.hh:494-534,
+ * 606-620). */
+int kh_group_consume_bytes_fixed_device(kh_group *grp, const uint8_t *const *d_bytes, uint64_t nreads,
+                                        uint64_t read_len);
+/* Hashtable::get_median_count (src/oxli/hashtable.cc:299-328) over every
+ * rank's own fixed-length reads (collective; 2-bit groups: packed words,
+ * Murmur groups: ASCII bytes; read_len - k + 1 <= 256).  A k-mer's bins live
+ * on several ranks: exchange mode routes each (k-mer, table) lookup to the
+ * bin's owner with the consume's level-1 partition and reduces the per-k-mer
+ * minima back (MIN reduce-scatter); broadcast mode has every rank take the
+ * minimum over its own bins of every source's k-mers (MIN reduce to the
+ * source).  The read's home rank computes median / average / stddev
+ * (float32 bit-exact as kh_median_counts_fixed_device) into d_med[l] /
+ * d_avg[l] / d_sd[l] (device, one entry per read of local shard l). */
+int kh_group_median_fixed_device(kh_group *grp, const void *const *d_reads, uint64_t nreads, uint64_t read_len,
+                                 uint16_t *const *d_med, float *const *d_avg, float *const *d_sd);
 
 #ifdef __cplusplus
 }

@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
         block_sync();
         PH(0);
         // records: the prefetched batch, then APPLY_RECS loads in flight per thread
-        if (!(P.ablate & 2)) {
+        if (!(KH_ABL(P, 2))) {
             // two batches of APPLY_RECS loads in flight: batch k+1 is issued
             // before batch k's atomics, so each wait is for the older batch only
             const uint64_t step = (uint64_t)(APPLY_RECS / 2) * TH;   // pairs
@@ -332,7 +332,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
                 if (c == 0) win |= 1u << k;
                 else inval |= 1u << k;
                 if (bigc && c == 255) full |= 1u << k;
-                if (bigc && c < 255 && v > 255 && !(P.ablate & 8)) {   // insert r sees c + r: full iff c + r >= 255, r < n
+                if (bigc && c < 255 && v > 255 && !(KH_ABL(P, 8))) {   // insert r sees c + r: full iff c + r >= 255, r < n
                     const uint32_t idx = atomicAdd(&s_flag[1], 1u);
                     A.xent[ri.e0 + idx] = ((o + k) << 8) | c;
                 }
@@ -367,13 +367,13 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
                 atomicOr(&chg[g >> 7], bits << ((g >> 2) & 31));
             }
         }
-        if (P.ablate & 1) nw = 0;
+        if (KH_ABL(P, 1)) nw = 0;
         PH(4);
         // changed 16-bin chunks back to the table; the rare full255 re-read
         auto write_back = [&]() {
             // pass 2: write back changed 16-bin chunks; winners to the region's segment
             for (uint32_t x = t; x < nchunk; x += blockDim.x) {
-                if (!((chg[x >> 5] >> (x & 31)) & 1) || (P.ablate & 4)) continue;
+                if (!((chg[x >> 5] >> (x & 31)) & 1) || (KH_ABL(P, 4))) continue;
                 const uint4 cv = ((const uint4 *)c0)[x];
                 if (KIND == BYTE) {
                     ((uint4 *)(tab + ri.bin_lo))[x] = cv;
@@ -447,7 +447,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
             const uint32_t st0 = incl - cc;
             const uint32_t wall = __shfl(incl, 63, 64);
             unsigned long long my_gb = 0;
-            if (t < 64 && cc && !(P.ablate & 512)) my_gb = atomicAdd(&A.cw_cur[t], (unsigned long long)cc);   // 512: timing only
+            if (t < 64 && cc && !(KH_ABL(P, 512))) my_gb = atomicAdd(&A.cw_cur[t], (unsigned long long)cc);   // 512: timing only
             PH(7);
             uint32_t *wst = cnt;
 #pragma unroll
@@ -658,7 +658,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_bit(Params P, ApplyArgs A) {
             }
             const uint32_t st0 = incl - cc;
             unsigned long long my_gb = 0;
-            if (t < 64 && cc && !(P.ablate & 512)) my_gb = atomicAdd(&A.cw_cur[t], (unsigned long long)cc);   // 512: timing only
+            if (t < 64 && cc && !(KH_ABL(P, 512))) my_gb = atomicAdd(&A.cw_cur[t], (unsigned long long)cc);   // 512: timing only
 #pragma unroll 2
             for (int u = 0; u < BPT; u++) {
                 const uint32_t o = t + (uint32_t)u * TH;

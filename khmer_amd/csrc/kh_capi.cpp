@@ -1487,6 +1487,32 @@ extern "C" int kh_group_consume_packed_fixed_device(kh_group *grp, const uint64_
     });
 }
 
+extern "C" int kh_group_consume_bytes_fixed_device(kh_group *grp, const uint8_t *const *d_bytes, uint64_t nreads,
+                                                   uint64_t read_len) {
+    return guard([&] {
+        CHECK_PTR(grp);
+        CHECK_PTR(d_bytes);
+        std::vector<std::unique_lock<std::recursive_mutex>> locks;
+        for (int l = 0; l < group_nlocal(grp->G); l++) locks.emplace_back(group_shard(grp->G, l)->mu);
+        group_consume_bytes_fixed(grp->G, d_bytes, nreads, read_len);
+    });
+}
+
+extern "C" int kh_group_median_fixed_device(kh_group *grp, const void *const *d_reads, uint64_t nreads,
+                                            uint64_t read_len, uint16_t *const *d_med, float *const *d_avg,
+                                            float *const *d_sd) {
+    return guard([&] {
+        CHECK_PTR(grp);
+        CHECK_PTR(d_reads);
+        CHECK_PTR(d_med);
+        CHECK_PTR(d_avg);
+        CHECK_PTR(d_sd);
+        std::vector<std::unique_lock<std::recursive_mutex>> locks;
+        for (int l = 0; l < group_nlocal(grp->G); l++) locks.emplace_back(group_shard(grp->G, l)->mu);
+        group_median_fixed(grp->G, d_reads, nreads, read_len, d_med, d_avg, d_sd);
+    });
+}
+
 extern "C" int kh_group_counters(kh_group *grp, uint64_t *n_unique, uint64_t *n_occupied) {
     return guard([&] {
         CHECK_PTR(grp);

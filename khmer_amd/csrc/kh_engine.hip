@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <type_traits>
 #include <vector>
 
@@ -265,9 +266,66 @@ static int env_seg(const char *name, int dflt) {   // development knobs (INTEGRA
 }
 static bool use_own_filter(const Graph *g);
 static size_t lds_window(bool window, int tile_kmers);
+static int l1f_tables_per_launch();
+
+// Level-1 launch windows.  k_scatter_l1f keeps per-bucket state in LDS for at
+// most 1024 buckets; a geometry with more (C4 / C5: 4 x 8e9 bins = 1908
+// buckets of 2^24 bins) runs one launch per group of consecutive tables whose
+// buckets [bb0, bb0 + nb) number at most KH_L1_WIN (default 1024).  Every
+// table starts on a bucket boundary (graph_prepare_params), so a group's
+// buckets are contiguous and each launch fills its own range of the bucket
+// buffer; the launch sees them as buckets 0 .. nb - 1 through a Params copy
+// whose table bases are shifted down by bb0 buckets (win_params).  Each
+// launch re-reads and re-hashes the k-mers (the 2-bit hash is ~3 % of level
+// 1; Murmur sources are hashed once into a u64 array first, pass_stage_a).
+struct L1Win {
+    int t0, nt;
+    uint32_t bb0, nb;
+};
+// Measured (C4 / C5 / C5M on one MI355X, profiles/r4_a): with the k-mers
+// of a 2-bit source re-hashed per launch, windows of 954 or 477 buckets take
+// 280 / 290 ms per step of level 1 against 195 for the exact two-pass level 1
+// (k_hist_l1 + k_scatter_l1), so multi-window level 1 is used only for
+// hashed-once sources (Murmur: 136 vs 151 ms at 477-bucket windows, 206 at
+// 954) and the exact path keeps the rest.  Windows of at most 512 buckets:
+// one table per launch at C4 / C5 / C5M.
+static uint32_t l1f_win_max() {
+    static const int v = [] {
+        const char *e = getenv("KH_L1_WIN");   // development A/B: buckets per launch
+        const int x = e && *e ? atoi(e) : 512;
+        return std::max(1, std::min(1024, x));
+    }();
+    return (uint32_t)v;
+}
+static std::vector<L1Win> l1f_windows(const Params &P, int tpl) {
+    const int shift = P.s0 + P.s2;
+    const uint32_t wmax = l1f_win_max();
+    auto bs = [&](int i) -> uint32_t { return (uint32_t)(P.tbase[i] >> shift); };
+    auto be = [&](int i) -> uint32_t { return i + 1 < P.n ? bs(i + 1) : P.F1; };
+    std::vector<L1Win> v;
+    if (P.F1 <= 1024 && P.n <= tpl) {   // one launch (C2: 240 buckets, C3: 956)
+        v.push_back({0, P.n, 0, P.F1});
+        return v;
+    }
+    for (int t0 = 0; t0 < P.n;) {
+        if (be(t0) - bs(t0) > 1024) return {};   // one table alone is too large
+        int nt = 1;
+        while (t0 + nt < P.n && nt < tpl && be(t0 + nt) - bs(t0) <= wmax) nt++;
+        v.push_back({t0, nt, bs(t0), std::max<uint32_t>(1, be(t0 + nt - 1) - bs(t0))});
+        t0 += nt;
+    }
+    return v;
+}
+static Params win_params(const Params &P, const L1Win &w) {
+    Params Q = P;
+    Q.F1 = w.nb;
+    const uint64_t sh = (uint64_t)w.bb0 << (P.s0 + P.s2);
+    for (int i = w.t0; i < w.t0 + w.nt; i++) Q.tbase[i] -= sh;
+    return Q;
+}
 static bool l1f_ok(const Graph *g) {
     static const bool off = [] { const char *e = getenv("KH_L1_EXACT"); return e && atoi(e); }();
-    return !off && g->prm.F1 <= 1024 && !use_own_filter(g);
+    return !off && !use_own_filter(g) && !l1f_windows(g->prm, l1f_tables_per_launch()).empty();
 }
 static uint32_t device_cus(const Graph *g) {
     static int cus[64] = {0};
@@ -317,10 +375,20 @@ static uint32_t l1f_wpc(const Params &P) {
     return (uint32_t)std::max<size_t>(1, std::min<size_t>(regs, 163840 / lds));
 }
 static bool use_own_filter(const Graph *g);
-static uint32_t l1f_workgroups(const Graph *g, uint64_t nkmers) {
+// workgroups of one level-1 launch over window geometry Q
+static uint32_t l1f_workgroups_q(const Graph *g, const Params &Q, uint64_t nkmers) {
     const uint64_t tiles = (nkmers + L1_THREADS - 1) / L1_THREADS;
-    const uint64_t wpc = use_own_filter(g) ? 2 : l1f_wpc(g->prm);   // k_own_l1f: ~75 KB of LDS
+    const uint64_t wpc = use_own_filter(g) ? 2 : l1f_wpc(Q);   // k_own_l1f: ~75 KB of LDS
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles / 8 + 1, wpc * device_cus(g)));
+}
+// the most workgroups any level-1 launch of the pass has (each leaves at most
+// one partial block per bucket it fills: bkt_plan's slack)
+static uint32_t l1f_workgroups(const Graph *g, uint64_t nkmers) {
+    if (use_own_filter(g)) return l1f_workgroups_q(g, g->prm, nkmers);
+    uint32_t m = 1;
+    for (const L1Win &w : l1f_windows(g->prm, l1f_tables_per_launch()))
+        m = std::max(m, l1f_workgroups_q(g, win_params(g->prm, w), nkmers));
+    return m;
 }
 static size_t lds_own_l1f(const Params &P) {
     const size_t F1a = (P.F1 + 3) & ~3u;
@@ -558,7 +626,7 @@ static void move_kstats(Graph *dst, Graph *src) {
 
 // level-1 scatter instance for a tail mode and k-mers per thread (8 / nt)
 template <class Src>
-using L1Fn = void (*)(Params, Src, uint64_t, uint32_t, uint32_t, int, int, uint64_t *, uint64_t *);
+using L1Fn = void (*)(Params, Src, uint64_t, uint32_t, uint32_t, int, int, uint64_t *, uint64_t *, uint32_t);
 template <class Src>
 static L1Fn<Src> l1_kernel(bool seg, int kpt) {
     switch (kpt) {
@@ -675,6 +743,66 @@ static uint64_t own_filter(Graph *g, const Src &src, uint64_t nkmers, bool windo
         if (cnt <= w.cap_frec) return cnt;
         if (attempt) fail(KH_EDEVICE, "owned-record filter overflowed twice");
         ensure((void **)&w.frec, &w.cap_frec, cnt, 8);
+    }
+}
+
+// register-direct level 1 (k_scatter_l1r): KH_L1R=1 (two 1024-thread
+// workgroups per CU, <= 64 VGPRs), 2 (one per CU), 0 off
+static int l1r_mode() { static const int v = env_seg("KH_L1R", 0); return v; }
+static size_t lds_scatter_l1r(const Params &P) { return (size_t)P.F1 * (8 + 8 + 16 * 8 + 4 + 4 + 2) + 16 + 64; }
+template <class Src>
+static L1FFn<Src> l1r_kernel(int kpt, int mode) {
+    if (mode == 1) {
+        switch (kpt) {
+            case 1: return k_scatter_l1r<Src, 1, 8>;
+            case 2: return k_scatter_l1r<Src, 2, 8>;
+            case 4: return k_scatter_l1r<Src, 4, 8>;
+            default: return k_scatter_l1r<Src, 8, 8>;
+        }
+    }
+    switch (kpt) {
+        case 1: return k_scatter_l1r<Src, 1, 4>;
+        case 2: return k_scatter_l1r<Src, 2, 4>;
+        case 4: return k_scatter_l1r<Src, 4, 4>;
+        default: return k_scatter_l1r<Src, 8, 4>;
+    }
+}
+
+// k_scatter_l1f over every level-1 window (l1f_windows) of graph g's
+// geometry: records of k-mer j carry index jbase + j
+template <class Src>
+static void launch_l1f(Graph *g, const Src &src, uint64_t nkmers, bool window, uint32_t jbase) {
+    Workspace &w = g->ws;
+    const int rpt = l1f_rpt();
+    for (const L1Win &wn : l1f_windows(g->prm, l1f_tables_per_launch())) {
+        const Params Q = win_params(g->prm, wn);
+        const int l1r = l1r_mode();
+        if (l1r && !window && Q.F1 <= (uint32_t)L1R_MAX_F1) {
+            int kpt = 1;
+            while (kpt * 2 * wn.nt <= 8) kpt *= 2;
+            const uint64_t tk = (uint64_t)L1R_THREADS * kpt;
+            const uint64_t per_cu = std::min<uint64_t>(l1r == 1 ? 2 : 1, 163840 / lds_scatter_l1r(Q));
+            const uint32_t nwg = (uint32_t)std::max<uint64_t>(
+                1, std::min<uint64_t>((nkmers + tk - 1) / tk / 4 + 1, std::max<uint64_t>(1, per_cu) * device_cus(g)));
+            const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
+            KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, g->stream));
+            TIMED("scatter_l1", hipLaunchKernelGGL(l1r_kernel<Src>(kpt, l1r), dim3(nwg), dim3(L1R_THREADS),
+                                                   lds_scatter_l1r(Q), g->stream, Q, src, nkmers, kpw, wn.t0, wn.nt,
+                                                   w.bkt_base + wn.bb0, (unsigned long long *)w.bkt_cur + wn.bb0,
+                                                   w.rec1, w.ctr, l1f_blk_sh(), jbase, l1f_chunk_tiles(g)));
+            continue;
+        }
+        const uint32_t nwg = l1f_workgroups_q(g, Q, nkmers);
+        int kpt = 1;
+        while (kpt * 2 * wn.nt <= rpt) kpt *= 2;
+        const uint64_t tk = (uint64_t)L1_THREADS * kpt;
+        const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
+        KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, g->stream));   // the chunk queue's head
+        TIMED("scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt, !window && l1f_tw(src, kpt)), dim3(nwg),
+                                               dim3(L1_THREADS), lds_scatter_l1f(Q, window, (int)tk), g->stream, Q,
+                                               src, nkmers, kpw, wn.t0, wn.nt, w.bkt_base + wn.bb0,
+                                               (unsigned long long *)w.bkt_cur + wn.bb0, w.rec1, w.ctr, l1f_blk_sh(),
+                                               jbase, l1f_chunk_tiles(g)));
     }
 }
 
@@ -863,14 +991,15 @@ template <class Src>
 static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     if (nkmers > MAX_PASS_KMERS) fail(KH_EVALUE, "device batch too large (more than 3200 * 2^20 k-mers)");
     if constexpr (std::is_same<Src, SrcBytes>::value || std::is_same<Src, SrcTwoBit>::value) {
-        // Murmur (the costly hash) over more than 1024 level-1 buckets: the
-        // exact level 1 would hash every k-mer twice (histogram, scatter);
+        // Murmur (the costly hash) over more than one level-1 window (or the
+        // exact level 1, which hashes every k-mer twice: histogram, scatter):
         // hash once into a u64 array and run the partition over that.
-        // KH_HASH_ONCE=0 keeps the two hashings, =2 also hashes 2-bit
+        // KH_HASH_ONCE=0 keeps the repeated hashing, =2 also hashes 2-bit
         // sources once (development A/B).
         static const int once = env_seg("KH_HASH_ONCE", 1);
         const bool want = std::is_same<Src, SrcBytes>::value ? once != 0 : once == 2;
-        if (want && !l1f_ok(g) && !use_own_filter(g)) {
+        const bool multi = !l1f_ok(g) || l1f_windows(g->prm, l1f_tables_per_launch()).size() > 1;
+        if (want && multi && !use_own_filter(g)) {
             Workspace &w = g->ws;
             ensure((void **)&w.frec, &w.cap_frec, nkmers, 8);
             const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nkmers + 255) / 256, 4096));
@@ -921,7 +1050,8 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     bool l1f = false;
     uint64_t nrec = 0;   // records this pass writes (exact level 1 only)
     for (;;) {
-        l1f = fast && l1f_ok(g);
+        l1f = fast && l1f_ok(g) &&
+              (std::is_same<Src, SrcHashes>::value || l1f_windows(P, l1f_tables_per_launch()).size() == 1);
         const bool ownf = fast && !window && use_own_filter(g) && own_l1f_on();
         const uint64_t cap1 = (l1f || ownf) ? bkt_plan(g, nkmers) : 0;
         // level 1
@@ -944,25 +1074,10 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
             }
         } else if (l1f) {
             ensure_recs(g, std::max(cap1, cap2));
-            if (P.ablate & 16) KH_HIP(hipMemsetAsync(w.rec1, 0xFF, w.cap_recs * 8, st));   // timing only
+            if (KH_ABL(P, 16)) KH_HIP(hipMemsetAsync(w.rec1, 0xFF, w.cap_recs * 8, st));   // timing only
             hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)((F1 + 255) / 256)), dim3(256), 0, st, w.bkt_base,
                                (unsigned long long *)w.bkt_cur, (uint64_t)F1);
-            const uint32_t nwg = l1f_workgroups(g, nkmers);
-            const int tpl = l1f_tables_per_launch();
-            for (int t0 = 0; t0 < P.n; t0 += tpl) {
-                const int nt = std::min(tpl, P.n - t0);
-                const int rpt = l1f_rpt();
-                int kpt = 1;
-                while (kpt * 2 * nt <= rpt) kpt *= 2;
-                const uint64_t tk = (uint64_t)L1_THREADS * kpt;
-                const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
-                KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, st));   // the chunk queue's head
-                TIMED("scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt, !window && l1f_tw(src, kpt)),
-                                                       dim3(nwg), dim3(L1_THREADS),
-                                                       lds_scatter_l1f(P, window, (int)tk), st, P, src, nkmers, kpw,
-                                                       t0, nt, w.bkt_base, (unsigned long long *)w.bkt_cur, w.rec1,
-                                                       w.ctr, l1f_blk_sh(), 0u, l1f_chunk_tiles(g)));
-            }
+            launch_l1f(g, src, nkmers, window, 0u);
         } else if (use_own_filter(g)) {
             nrec = own_filter(g, src, nkmers, window);
             const uint32_t nch = (uint32_t)std::max<uint64_t>(1, (nrec + L2_CHUNK - 1) / L2_CHUNK);
@@ -985,7 +1100,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
             TIMED("scatter_l1", hipLaunchKernelGGL((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>),
                                                    dim3(nch), dim3(L1_THREADS),
                                                    lds_scatter_l1(P, false, L1_THREADS * L1_MAX_RPT), st, P, rs, nrec,
-                                                   (uint32_t)L2_CHUNK, nch, 0, 1, w.moff, w.rec1));
+                                                   (uint32_t)L2_CHUNK, nch, 0, 1, w.moff, w.rec1, 0u));
         } else {
             TIMED("hist_l1", hipLaunchKernelGGL(k_hist_l1<Src>, dim3(q.nch1), dim3(L1_THREADS), lds_hist_l1(P, window),
                                                 st, P, src, nkmers, q.ck1, q.nch1, w.mcnt));
@@ -1005,7 +1120,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
                 const int tile_kmers = L1_THREADS * kpt;
                 TIMED("scatter_l1", hipLaunchKernelGGL(l1_kernel<Src>(l1_seg(P) != 0, kpt), dim3(q.nch1),
                                                        dim3(L1_THREADS), lds_scatter_l1(P, window, tile_kmers), st, P,
-                                                       src, nkmers, q.ck1, q.nch1, t0, nt, w.moff, w.rec1));
+                                                       src, nkmers, q.ck1, q.nch1, t0, nt, w.moff, w.rec1, 0u));
             }
         }
         if (check_mode() && !l1f && !ownf) check_holes(g, w.rec1, nrec, "scatter_l1");
@@ -1602,10 +1717,11 @@ void graph_prepare_params(Graph *g) {
     P.k = g->k;
     P.n = g->n;
     P.use_bigcount = g->use_bigcount ? 1 : 0;
-    // KH_ABLATE: timing-only switches that skip work (wrong results); bench
-    // ablation studies only
+#ifdef KH_ABLATE
+    // timing-only switches that skip work (wrong results): development builds only
     const char *ab = getenv("KH_ABLATE");
     P.ablate = ab ? atoi(ab) : 0;
+#endif
     // regions of 2^14 bins (Byte/Nibble: 1024-thread apply, ~154 KiB of LDS;
     // KH_S0=13 selects the 2^13-bin, 512-thread variant)
     static const int s0_env = env_seg("KH_S0", 14);
@@ -1673,6 +1789,12 @@ static void set_lds_limits() {
         KH_LDS_MAX(l1f_kernel<SrcHashes>(kpt, 8));
     }
     KH_LDS_MAX((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>));
+    for (int kpt : {1, 2, 4, 8})
+        for (int mode : {1, 2}) {
+            KH_LDS_MAX(l1r_kernel<SrcTwoBit>(kpt, mode));
+            KH_LDS_MAX(l1r_kernel<SrcBytes>(kpt, mode));
+            KH_LDS_MAX(l1r_kernel<SrcHashes>(kpt, mode));
+        }
     for (int kpt : {1, 2, 4, 8}) {
         KH_LDS_MAX(own_l1f_kernel<SrcTwoBit>(kpt, false));
         KH_LDS_MAX(own_l1f_kernel<SrcTwoBit>(kpt, true));
@@ -1852,6 +1974,10 @@ struct ShardGroup {
         uint64_t cap_seg = 0;        // exchange mode: level-2 segment starts and ends
         uint64_t *slot[2] = {nullptr, nullptr};
         uint64_t cap_slot[2] = {0, 0};
+        uint8_t *q8 = nullptr;
+        uint64_t cap_q8 = 0;         // sharded query: per-k-mer minima (owner lookups / own bins)
+        uint8_t *o8 = nullptr;
+        uint64_t cap_o8 = 0;         // sharded query: the reduced minima of this rank's k-mers
         hipStream_t st_x = nullptr;
         hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
         bool freed[2] = {false, false};
@@ -1865,7 +1991,8 @@ struct ShardGroup {
             auto &lc = loc[l];
             if (lc.st_x) (void)hipStreamSynchronize(lc.st_x);
             for (void *p : {(void *)lc.src, (void *)lc.recv, (void *)lc.ws, (void *)lc.ws_all, (void *)lc.roff,
-                            (void *)lc.flist, (void *)lc.fall, (void *)lc.slot[0], (void *)lc.slot[1], (void *)lc.seg})
+                            (void *)lc.flist, (void *)lc.fall, (void *)lc.slot[0], (void *)lc.slot[1], (void *)lc.seg,
+                            (void *)lc.q8, (void *)lc.o8})
                 if (p) (void)hipFree(p);
             for (int b = 0; b < 2; b++) {
                 if (lc.ev_ready[b]) (void)hipEventDestroy(lc.ev_ready[b]);
@@ -1963,12 +2090,14 @@ static void group_make_shards(ShardGroup *G, int kind, int hash, int k, const ui
                               const int *devices, bool exchange) {
     const int world = G->world;
     if (exchange) {
-        if (hash != TWOBIT) fail(KH_EVALUE, "exchange mode takes 2-bit hashed graphs");
         for (int l = 0; l < G->nlocal; l++)
             G->views.push_back(graph_build(kind, hash, k, sizes, n, devices[l], 1, 0, nullptr, nullptr, -1, false));
         const Params &V = G->views[0]->prm;
         if (V.F1 < (uint32_t)world) fail(KH_EVALUE, "exchange mode needs at least one level-1 bucket per rank");
-        if (V.F1 > 1024) fail(KH_EVALUE, "exchange mode supports at most 1024 level-1 buckets");
+        // level 1 of the unsharded view runs in launch windows of <= 1024
+        // buckets (l1f_windows): any table of at most 1024 buckets (1.7e10 bins)
+        if (l1f_windows(V, l1f_tables_per_launch()).empty())
+            fail(KH_EVALUE, "exchange mode: a table has more than 1024 level-1 buckets");
         a2a_plan(V, sizes, n, world, G->B, G->blo, G->bhi);
         G->a2a = true;
     }
@@ -1992,7 +2121,9 @@ ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n
     G->rank0 = nlocal == world ? 0 : rank;
     group_make_shards(G.get(), kind, hash, k, sizes, n, devices, exchange != 0);
     G->loc.resize(nlocal);
-    if (nlocal == 1 && world > 1) {
+    // RCCL for one shard per process; a 1-rank group given a unique id runs
+    // every RCCL call site too (communicator creation, split, collectives)
+    if (nlocal == 1 && (world > 1 || uid)) {
         if (!uid) fail(KH_EVALUE, "an RCCL group needs the unique id of rank 0");
         ncclUniqueId id;
         memcpy(&id, uid, sizeof id);
@@ -2142,19 +2273,25 @@ static void group_merge_full_dense(ShardGroup *G, uint64_t nkb) {
         return;
     }
     if (G->hosted) {
+        // in slices of at most 256 MB: a rank holds W slices at a time, not W
+        // whole per-k-mer arrays (up to 3.3 GB each)
         Graph *g = G->shards[0];
         KH_HIP(hipSetDevice(g->device));
-        std::vector<uint8_t> mine(nkb), all((size_t)W * nkb);
-        KH_HIP(hipMemcpyAsync(mine.data(), g->ws.fullf, nkb, hipMemcpyDeviceToHost, g->stream));
-        KH_HIP(hipStreamSynchronize(g->stream));
-        host_rc(G->tp.allgather(G->tp.ctx, mine.data(), all.data(), nkb), "allgather");
-        for (uint64_t i = 0; i < nkb; i++) {
-            uint32_t v = 0;
-            for (int r = 0; r < W; r++) v += all[(size_t)r * nkb + i];
-            mine[i] = (uint8_t)v;
+        const uint64_t piece = std::min<uint64_t>(nkb, 256ull << 20);
+        std::vector<uint8_t> mine(piece), all((size_t)W * piece);
+        for (uint64_t a = 0; a < nkb; a += piece) {
+            const uint64_t n = std::min(piece, nkb - a);
+            KH_HIP(hipMemcpyAsync(mine.data(), g->ws.fullf + a, n, hipMemcpyDeviceToHost, g->stream));
+            KH_HIP(hipStreamSynchronize(g->stream));
+            host_rc(G->tp.allgather(G->tp.ctx, mine.data(), all.data(), n), "allgather");
+            for (uint64_t i = 0; i < n; i++) {
+                uint32_t v = 0;
+                for (int r = 0; r < W; r++) v += all[(size_t)r * n + i];
+                mine[i] = (uint8_t)v;
+            }
+            KH_HIP(hipMemcpyAsync(g->ws.fullf + a, mine.data(), n, hipMemcpyHostToDevice, g->stream));
+            KH_HIP(hipStreamSynchronize(g->stream));
         }
-        KH_HIP(hipMemcpyAsync(g->ws.fullf, mine.data(), nkb, hipMemcpyHostToDevice, g->stream));
-        KH_HIP(hipStreamSynchronize(g->stream));
         return;
     }
     // loopback: sum every shard's array into shard 0's, then copy it back out
@@ -2268,29 +2405,59 @@ static void a2a_level1(Graph *V, const Src &src, uint64_t nkmers, uint32_t jbase
     const Params &P = V->prm;
     Workspace &w = V->ws;
     hipStream_t st = V->stream;
-    ws_prepare(V, pass_geo(P, nkmers));
+    if constexpr (std::is_same<Src, SrcBytes>::value) {
+        // Murmur over several level-1 windows: hash once (as pass_stage_a)
+        if (l1f_windows(P, l1f_tables_per_launch()).size() > 1) {
+            ensure((void **)&w.frec, &w.cap_frec, nkmers, 8);
+            const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nkmers + 255) / 256, 4096));
+            TIMED_G(V, "hash", hipLaunchKernelGGL(k_hash_kmers<Src>, dim3(grid), dim3(256), 0, st, src, nkmers,
+                                                  w.frec));
+            KH_HIP(hipGetLastError());
+            SrcHashes hs{};
+            static_cast<SrcCommon &>(hs) = static_cast<const SrcCommon &>(src);
+            hs.koff = nullptr;
+            hs.kpr = 0;
+            hs.kbase = 0;
+            hs.h = w.frec;
+            a2a_level1(V, hs, nkmers, jbase);
+            return;
+        }
+    }
+    const PassGeo q = pass_geo(P, nkmers);
+    ws_prepare(V, q);
     const uint64_t F1 = P.F1;
+    w.l1_exact = !std::is_same<Src, SrcHashes>::value && l1f_windows(P, l1f_tables_per_launch()).size() > 1;
+    if (w.l1_exact) {
+        // more than 1024 buckets (C4 / C5 tables): the exact two-pass level 1
+        // (as pass_stage_a) -- bucket b's records are [off1[b], off1[b + 1])
+        KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
+        TIMED_G(V, "hist_l1", hipLaunchKernelGGL(k_hist_l1<Src>, dim3(q.nch1), dim3(L1_THREADS),
+                                                 lds_hist_l1(P, false), st, P, src, nkmers, q.ck1, q.nch1, w.mcnt));
+        TIMED_G(V, "scan", scan_counts(V, w.mcnt, w.moff, F1 * q.nch1));
+        TIMED_G(V, "plan_l2", hipLaunchKernelGGL(k_plan_l2, dim3(1), dim3(1024), F1 * 8 + 1025 * 8, st, (uint32_t)F1,
+                                                 q.nch1, w.moff, w.mcnt, w.off1, w.ch2));
+        uint64_t nrec = 0;
+        KH_HIP(hipMemcpyAsync(&nrec, w.off1 + F1, 8, hipMemcpyDeviceToHost, st));
+        KH_HIP(hipStreamSynchronize(st));
+        ensure_recs(V, nrec, false);
+        for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
+            const int nt = std::min(L1_MAX_RPT, P.n - t0);
+            const int kpt = std::max(1, L1_MAX_RPT / nt);
+            TIMED_G(V, "scatter_l1", hipLaunchKernelGGL(l1_kernel<Src>(l1_seg(P) != 0, kpt), dim3(q.nch1),
+                                                        dim3(L1_THREADS), lds_scatter_l1(P, false, L1_THREADS * kpt),
+                                                        st, P, src, nkmers, q.ck1, q.nch1, t0, nt, w.moff, w.rec1,
+                                                        jbase));
+        }
+        KH_HIP(hipGetLastError());
+        return;
+    }
     for (;;) {
         const uint64_t cap1 = bkt_plan(V, nkmers);
         ensure_recs(V, cap1, false);
         KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
         hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)((F1 + 255) / 256)), dim3(256), 0, st, w.bkt_base,
                            (unsigned long long *)w.bkt_cur, (uint64_t)F1);
-        const uint32_t nwg = l1f_workgroups(V, nkmers);
-        for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
-            const int nt = std::min(L1_MAX_RPT, P.n - t0);
-            const int rpt = l1f_rpt();
-            int kpt = 1;
-            while (kpt * 2 * nt <= rpt) kpt *= 2;
-            const uint64_t tk = (uint64_t)L1_THREADS * kpt;
-            const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
-            KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, st));   // the chunk queue's head
-            TIMED_G(V, "scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt, l1f_tw(src, kpt)), dim3(nwg),
-                                                        dim3(L1_THREADS), lds_scatter_l1f(P, false, (int)tk), st, P,
-                                                        src, nkmers, kpw, t0, nt, w.bkt_base,
-                                                        (unsigned long long *)w.bkt_cur, w.rec1, w.ctr, l1f_blk_sh(),
-                                                        jbase, l1f_chunk_tiles(V)));
-        }
+        launch_l1f(V, src, nkmers, false, jbase);
         uint64_t err = 0;
         KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
         KH_HIP(hipStreamSynchronize(st));
@@ -2314,8 +2481,13 @@ static void a2a_meta(ShardGroup *G, std::vector<uint64_t> &meta) {
         Graph *V = G->views[l];
         KH_HIP(hipSetDevice(V->device));
         uint64_t *h = meta.data() + (size_t)(G->rank0 + l) * M;
-        KH_HIP(hipMemcpyAsync(h, V->ws.bkt_base, (F1 + 1) * 8, hipMemcpyDeviceToHost, V->stream));
-        KH_HIP(hipMemcpyAsync(h + F1 + 1, V->ws.bkt_cur, F1 * 8, hipMemcpyDeviceToHost, V->stream));
+        if (V->ws.l1_exact) {   // exact level 1: contiguous buckets, ends = the next bucket's start
+            KH_HIP(hipMemcpyAsync(h, V->ws.off1, (F1 + 1) * 8, hipMemcpyDeviceToHost, V->stream));
+            KH_HIP(hipMemcpyAsync(h + F1 + 1, V->ws.off1 + 1, F1 * 8, hipMemcpyDeviceToHost, V->stream));
+        } else {
+            KH_HIP(hipMemcpyAsync(h, V->ws.bkt_base, (F1 + 1) * 8, hipMemcpyDeviceToHost, V->stream));
+            KH_HIP(hipMemcpyAsync(h + F1 + 1, V->ws.bkt_cur, F1 * 8, hipMemcpyDeviceToHost, V->stream));
+        }
         KH_HIP(hipStreamSynchronize(V->stream));
         h[2 * F1 + 1] = h[F1];
     }
@@ -2404,29 +2576,14 @@ static void a2a_exchange(ShardGroup *G, const std::vector<uint64_t> &meta, std::
     }
 }
 
-// the owner's level 2 over its (source, bucket) segments, apply and winners
-static PassState a2a_owner_pass(ShardGroup *G, int l, const std::vector<uint64_t> &meta,
-                                const std::vector<uint64_t> &rb, uint64_t nk) {
+// the owner's received records as W * NB segments (lc.seg: starts, then
+// ends): segment s * NB + b = source s's bucket B[r] + b inside its block of
+// rec1.  Returns the number of segments.
+static uint64_t a2a_segments(ShardGroup *G, int l, const std::vector<uint64_t> &meta, const std::vector<uint64_t> &rb) {
     const int W = G->world, r = G->rank0 + l;
     Graph *g = G->shards[l];
-    const Params &P = g->prm;
-    Workspace &w = g->ws;
-    hipStream_t st = g->stream;
-    KH_HIP(hipSetDevice(g->device));
     const uint64_t F1v = G->views[0]->prm.F1, M = 2 * (F1v + 1);
     const uint32_t NB = G->B[r + 1] - G->B[r];
-    if (NB != P.F1) fail(KH_EDEVICE, "exchange mode: owner geometry does not match its bucket range");
-    PassState ps;
-    ps.q = pass_geo(P, nk);
-    ps.nkmers = nk;
-    ps.bigc = P.kind == BYTE && P.use_bigcount;
-    ws_prepare(g, ps.q);
-    KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
-    if (ps.bigc) {
-        KH_HIP(hipMemsetAsync(w.fullf, 0, (nk + 15) & ~15ull, st));
-        bcmap_clear(w, st);
-    }
-    // segment s * NB + b: source s's bucket B[r] + b inside its block of rec1
     const uint64_t nseg = (uint64_t)W * NB;
     std::vector<uint64_t> seg(2 * (nseg + 1));
     for (int s = 0; s < W; s++)
@@ -2440,7 +2597,33 @@ static PassState a2a_owner_pass(ShardGroup *G, int l, const std::vector<uint64_t
     seg[2 * nseg + 1] = rb[W];
     auto &lc = G->loc[l];
     ensure((void **)&lc.seg, &lc.cap_seg, 2 * (nseg + 1), 8);
-    KH_HIP(hipMemcpyAsync(lc.seg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, st));
+    KH_HIP(hipMemcpyAsync(lc.seg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, g->stream));
+    return nseg;
+}
+
+// the owner's level 2 over its (source, bucket) segments, apply and winners
+static PassState a2a_owner_pass(ShardGroup *G, int l, const std::vector<uint64_t> &meta,
+                                const std::vector<uint64_t> &rb, uint64_t nk) {
+    const int W = G->world, r = G->rank0 + l;
+    Graph *g = G->shards[l];
+    const Params &P = g->prm;
+    Workspace &w = g->ws;
+    hipStream_t st = g->stream;
+    KH_HIP(hipSetDevice(g->device));
+    const uint32_t NB = G->B[r + 1] - G->B[r];
+    if (NB != P.F1) fail(KH_EDEVICE, "exchange mode: owner geometry does not match its bucket range");
+    PassState ps;
+    ps.q = pass_geo(P, nk);
+    ps.nkmers = nk;
+    ps.bigc = P.kind == BYTE && P.use_bigcount;
+    ws_prepare(g, ps.q);
+    KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
+    if (ps.bigc) {
+        KH_HIP(hipMemsetAsync(w.fullf, 0, (nk + 15) & ~15ull, st));
+        bcmap_clear(w, st);
+    }
+    const uint64_t nseg = a2a_segments(G, l, meta, rb);
+    auto &lc = G->loc[l];
     const uint64_t F2 = 1ull << P.s2, nreg = (uint64_t)P.F1 * F2;
     // W segments per bucket: split each into parts / W so a region has as many
     // writing workgroups (partial blocks) as reg_plan's slack allows
@@ -2484,8 +2667,9 @@ static PassState a2a_owner_pass(ShardGroup *G, int l, const std::vector<uint64_t
 // finalize of the own chunk (its k-mers are [r * stride, r * stride + nkc) of
 // the pass), counters, and the bigcount events of every rank merged into
 // every rank's map (ByteStorage::add's saturating sum is order-free)
-static void a2a_stage_c(ShardGroup *G, std::vector<PassState> &ps, const std::vector<SrcTwoBit> &srcs,
-                        uint64_t stride, uint64_t nkc) {
+template <class Src>
+static void a2a_stage_c(ShardGroup *G, std::vector<PassState> &ps, const std::vector<Src> &srcs, uint64_t stride,
+                        uint64_t nkc) {
     const int W = G->world, NL = G->nlocal;
     std::vector<std::vector<uint64_t>> keys(W);
     std::vector<std::vector<uint32_t>> cnts(W);
@@ -2502,7 +2686,7 @@ static void a2a_stage_c(ShardGroup *G, std::vector<PassState> &ps, const std::ve
         const unsigned fgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nchunk + FIN_THREADS - 1) / FIN_THREADS, 4096));
         for (;;) {
             if (bigc)
-                TIMED("finalize", hipLaunchKernelGGL(k_finalize<SrcTwoBit>, dim3(fgrid), dim3(FIN_THREADS), 0, st, P,
+                TIMED("finalize", hipLaunchKernelGGL(k_finalize<Src>, dim3(fgrid), dim3(FIN_THREADS), 0, st, P,
                                                      srcs[l], nkc, w.fullf + (uint64_t)r * stride, w.ctr, w.bck, w.bcv,
                                                      w.cap_bcmap - 1, (uint64_t *)nullptr));
             KH_HIP(hipGetLastError());
@@ -2590,52 +2774,119 @@ static void a2a_stage_c(ShardGroup *G, std::vector<PassState> &ps, const std::ve
     }
 }
 
-static void group_consume_a2a(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len) {
+// A group consume call's input: every rank's own fixed-length reads, packed
+// 2-bit words (2-bit hashed graphs) or ASCII bytes (the Murmur-hashed
+// Counttable family), the same count and length on every rank.
+struct GroupReads {
+    bool bytes = false;
+    const void *const *d = nullptr;   // one device buffer per local shard
+    uint64_t nreads = 0, read_len = 0, kpr = 0;
+    // broadcast units (u64 words or bytes) of one rank's reads
+    uint64_t units() const { return bytes ? nreads * read_len : (nreads * read_len + 31) / 32 + 1; }
+    size_t esize() const { return bytes ? 1 : 8; }
+    ncclDataType_t nccl_type() const { return bytes ? ncclUint8 : ncclUint64; }
+};
+
+// the source of reads [r0, r0 + nr) of buffer `buf` (a rank's reads) for graph g
+template <class Src>
+static Src group_src(Graph *g, const GroupReads &R, const void *buf, uint64_t r0, uint64_t nr);
+template <>
+SrcTwoBit group_src<SrcTwoBit>(Graph *g, const GroupReads &R, const void *buf, uint64_t r0, uint64_t nr) {
+    SrcTwoBit s = src_twobit(g, (const uint64_t *)buf);
+    set_fixed(s, R.kpr);
+    s.koff = nullptr;
+    s.nreads = nr;
+    s.kbase = r0 * R.kpr;
+    s.rbase = 0;
+    return s;
+}
+template <>
+SrcBytes group_src<SrcBytes>(Graph *g, const GroupReads &R, const void *buf, uint64_t r0, uint64_t nr) {
+    // the windows read up to 64 bytes past the pass's last read (padded_bytes);
+    // the pass's reverse-complement stream goes to g's workspace
+    const uint8_t *b = padded_bytes(g, (const uint8_t *)buf + r0 * R.read_len, nr * R.read_len);
+    SrcBytes s = src_bytes(g, b, nullptr, nr, R.kpr, nr * R.read_len);
+    set_fixed(s, R.kpr);
+    s.koff = nullptr;
+    s.nreads = nr;
+    s.kbase = 0;
+    s.rbase = 0;
+    return s;
+}
+
+// Pass-level failure agreement (collective).  In a one-shard-per-process
+// group a rank that fails on its own (a capacity overflow at the largest
+// margin, an allocation failure) would leave its peers blocked in the pass's
+// next collective; instead every rank reaches this point, the error flags are
+// all-reduced, and all ranks fail together.  Loopback: rethrow directly.
+static void group_agree(ShardGroup *G, std::exception_ptr err) {
+    if (per_rank(G) && G->world > 1) {
+        Graph *g = G->shards[0];
+        KH_HIP(hipSetDevice(g->device));
+        const uint64_t mine = err ? 1 : 0;
+        uint64_t any = 0;
+        KH_HIP(hipMemcpyAsync(G->d_red + 170, &mine, 8, hipMemcpyHostToDevice, g->stream));
+        coll_allreduce_u64(G, g->stream, G->d_red + 170, G->d_red + 171, 1, RED_MAX);
+        KH_HIP(hipMemcpyAsync(&any, G->d_red + 171, 8, hipMemcpyDeviceToHost, g->stream));
+        KH_HIP(hipStreamSynchronize(g->stream));
+        if (any && !err) fail(KH_EDEVICE, "sharded consume: another rank failed in this pass");
+    }
+    if (err) std::rethrow_exception(err);
+}
+#define GROUP_TRY(...)                                                                             \
+    do {                                                                                           \
+        std::exception_ptr e_;                                                                     \
+        try { __VA_ARGS__; } catch (...) { e_ = std::current_exception(); }                        \
+        group_agree(G, e_);                                                                        \
+    } while (0)
+
+// Exchange-mode passes: a pass takes the next rpb reads of every rank; its
+// k-mer index space W * stride (stride a multiple of 16: fullf chunks) stays
+// below 2^32 (khmer_amd.parallel.exchange_passes restates this plan)
+static void a2a_pass_plan(ShardGroup *G, Graph *g0, const GroupReads &R, uint64_t *rpb, uint64_t *stride) {
+    const uint64_t cap = std::min<uint64_t>(g0->batch_kmers, MAX_PASS_KMERS) / (uint64_t)G->world;
+    const uint64_t rpb0 = std::max<uint64_t>(1, (cap > 16 ? cap - 16 : 1) / R.kpr);
+    const uint64_t npass = std::max<uint64_t>(1, (R.nreads + rpb0 - 1) / rpb0);
+    *rpb = std::max<uint64_t>(1, (R.nreads + npass - 1) / npass);
+    *stride = (*rpb * R.kpr + 15) & ~15ull;
+}
+
+template <class Src>
+static void group_consume_a2a(ShardGroup *G, const GroupReads &R) {
     const int W = G->world, NL = G->nlocal;
     Graph *g0 = G->shards[0];
-    const uint64_t kpr = read_len - g0->k + 1;
-    // a pass: the next rpb reads of every rank; its k-mer index space W *
-    // stride (stride a multiple of 16: fullf chunks) stays below 2^32
-    const uint64_t cap = std::min<uint64_t>(g0->batch_kmers, MAX_PASS_KMERS) / (uint64_t)W;
-    const uint64_t rpb0 = std::max<uint64_t>(1, (cap > 16 ? cap - 16 : 1) / kpr);
-    const uint64_t npass = std::max<uint64_t>(1, (nreads + rpb0 - 1) / rpb0);
-    const uint64_t rpb = std::max<uint64_t>(1, (nreads + npass - 1) / npass);
-    const uint64_t stride = (rpb * kpr + 15) & ~15ull;
+    const uint64_t kpr = R.kpr, nreads = R.nreads;
+    uint64_t rpb, stride;
+    a2a_pass_plan(G, g0, R, &rpb, &stride);
     const uint64_t nk = (uint64_t)W * stride;
     for (uint64_t r0 = 0; r0 < nreads; r0 += rpb) {
         const uint64_t nr = std::min(rpb, nreads - r0), nkc = nr * kpr;
-        std::vector<SrcTwoBit> srcs(NL);
-        for (int l = 0; l < NL; l++) {
+        std::vector<Src> srcs(NL);
+        GROUP_TRY(for (int l = 0; l < NL; l++) {
             Graph *V = G->views[l];
             KH_HIP(hipSetDevice(V->device));
             V->use_bigcount = false;   // the owners finalize; the view only runs level 1
             V->profile = G->shards[l]->profile;
-            SrcTwoBit sb = src_twobit(V, d_words[l]);
-            set_fixed(sb, kpr);
-            sb.koff = nullptr;
-            sb.nreads = nr;
-            sb.kbase = r0 * kpr;
-            sb.rbase = 0;
-            srcs[l] = sb;
-            a2a_level1(V, sb, nkc, (uint32_t)((uint64_t)(G->rank0 + l) * stride));
+            srcs[l] = group_src<Src>(V, R, R.d[l], r0, nr);
+            a2a_level1(V, srcs[l], nkc, (uint32_t)((uint64_t)(G->rank0 + l) * stride));
             move_kstats(G->shards[l], V);
-        }
+        });
         std::vector<uint64_t> meta;
         a2a_meta(G, meta);
         // owner buffers: the received records (level 1) and the level-2 regions
         const uint64_t F1v = G->views[0]->prm.F1, M = 2 * (F1v + 1);
-        for (int l = 0; l < NL; l++) {
+        GROUP_TRY(for (int l = 0; l < NL; l++) {
             const int r = G->rank0 + l;
             Graph *g = G->shards[l];
             KH_HIP(hipSetDevice(g->device));
             uint64_t need = 0;
             for (int s = 0; s < W; s++) need += meta[(size_t)s * M + G->B[r + 1]] - meta[(size_t)s * M + G->B[r]];
             ensure_recs(g, std::max(need, reg_plan(g, nk)));
-        }
+        });
         std::vector<std::vector<uint64_t>> rb;
         a2a_exchange(G, meta, rb);
         std::vector<PassState> ps(NL);
-        for (int l = 0; l < NL; l++) ps[l] = a2a_owner_pass(G, l, meta, rb[l], nk);
+        GROUP_TRY(for (int l = 0; l < NL; l++) ps[l] = a2a_owner_pass(G, l, meta, rb[l], nk));
         group_route_winners(G, ps);
         if (ps[0].bigc) group_merge_full(G, ps);
         a2a_stage_c(G, ps, srcs, stride, nkc);
@@ -2647,32 +2898,15 @@ static void group_consume_a2a(ShardGroup *G, const uint64_t *const *d_words, uin
     }
 }
 
-// collective: every rank passes its own fixed-length packed reads (same
-// count and length on every rank); consumed as the stream rank 0, 1, ...
-void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len) {
+// the broadcast-mode consume (Option B) of every rank's reads, source by source
+template <class Src>
+static void group_consume_bcast(ShardGroup *G, const GroupReads &R) {
     const int W = G->world, NL = G->nlocal;
     Graph *g0 = G->shards[0];
-    const int k = g0->k;
-    if (g0->hash != TWOBIT) fail(KH_EVALUE, "sharded consume takes 2-bit packed reads");
-    if (read_len < (uint64_t)k) fail(KH_EVALUE, "reads shorter than k");
-    if (per_rank(G)) {
-        // every rank must pass the same shape (collective schedule depends on it)
-        uint64_t h[2] = {nreads, read_len};
-        KH_HIP(hipSetDevice(g0->device));
-        KH_HIP(hipMemcpyAsync(G->d_red + 140, h, 16, hipMemcpyHostToDevice, g0->stream));
-        coll_allreduce_u64(G, g0->stream, G->d_red + 140, G->d_red + 142, 2, RED_MAX);
-        coll_allreduce_u64(G, g0->stream, G->d_red + 140, G->d_red + 144, 2, RED_MIN);
-        uint64_t mm[4];
-        KH_HIP(hipMemcpyAsync(mm, G->d_red + 142, 32, hipMemcpyDeviceToHost, g0->stream));
-        KH_HIP(hipStreamSynchronize(g0->stream));
-        if (mm[0] != mm[2] || mm[1] != mm[3]) fail(KH_EVALUE, "ranks passed different read counts or lengths");
-    }
-    if (G->a2a) {
-        group_consume_a2a(G, d_words, nreads, read_len);
-        return;
-    }
-    const uint64_t kpr = read_len - k + 1;
-    const uint64_t nwords = (nreads * read_len + 31) / 32 + 1;
+    const uint64_t kpr = R.kpr, nreads = R.nreads;
+    const uint64_t nunits = R.units();
+    const size_t esz = R.esize();
+    const uint64_t slot_words = (nunits * esz + 64 + 7) / 8;   // + the windows' 64-byte read-ahead
     const uint64_t rpb0 = std::max<uint64_t>(1, std::min<uint64_t>(g0->batch_kmers, MAX_PASS_KMERS) / kpr);
     const uint64_t npass = std::max<uint64_t>(1, (nreads + rpb0 - 1) / rpb0);
     const uint64_t rpb = std::max<uint64_t>(1, (nreads + npass - 1) / npass);   // equal passes
@@ -2701,30 +2935,30 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
             const int b = s & 1;
             KH_HIP(hipSetDevice(G->shards[l]->device));
             if (lc.freed[b]) KH_HIP(hipStreamWaitEvent(lc.st_x, lc.ev_free[b], 0));
+            if (!own(s, l)) {
+                if (lc.cap_slot[b] < slot_words) KH_HIP(hipStreamSynchronize(lc.st_x));   // about to be reallocated
+                ensure((void **)&lc.slot[b], &lc.cap_slot[b], slot_words, 8);
+                KH_HIP(hipMemsetAsync((uint8_t *)lc.slot[b] + nunits * esz, 0, 64, lc.st_x));
+            }
             if (G->hosted) {
                 // synchronous: the root's reads through host memory into the slot
-                std::vector<uint64_t> hb(nwords);
+                std::vector<uint8_t> hb(nunits * esz);
                 if (own(s, l)) {
                     KH_HIP(hipStreamSynchronize(G->shards[l]->stream));
-                    KH_HIP(hipMemcpy(hb.data(), d_words[0], nwords * 8, hipMemcpyDeviceToHost));
+                    KH_HIP(hipMemcpy(hb.data(), R.d[0], hb.size(), hipMemcpyDeviceToHost));
                 }
-                host_rc(G->tp.broadcast(G->tp.ctx, hb.data(), nwords * 8, s), "broadcast");
+                host_rc(G->tp.broadcast(G->tp.ctx, hb.data(), hb.size(), s), "broadcast");
                 if (!own(s, l)) {
-                    KH_HIP(hipStreamSynchronize(lc.st_x));
-                    ensure((void **)&lc.slot[b], &lc.cap_slot[b], nwords, 8);
-                    KH_HIP(hipMemcpyAsync(lc.slot[b], hb.data(), nwords * 8, hipMemcpyHostToDevice, lc.st_x));
+                    KH_HIP(hipMemcpyAsync(lc.slot[b], hb.data(), hb.size(), hipMemcpyHostToDevice, lc.st_x));
                     KH_HIP(hipStreamSynchronize(lc.st_x));
                 }
             } else if (own(s, l)) {
-                uint64_t *w = const_cast<uint64_t *>(d_words[0]);
-                KH_NCCL(ncclBroadcast(w, w, nwords, ncclUint64, s, G->comm_b, lc.st_x));
+                void *w = const_cast<void *>(R.d[0]);
+                KH_NCCL(ncclBroadcast(w, w, nunits, R.nccl_type(), s, G->comm_b, lc.st_x));
+            } else if (rccl) {
+                KH_NCCL(ncclBroadcast(lc.slot[b], lc.slot[b], nunits, R.nccl_type(), s, G->comm_b, lc.st_x));
             } else {
-                if (lc.cap_slot[b] < nwords) KH_HIP(hipStreamSynchronize(lc.st_x));   // slot about to be reallocated
-                ensure((void **)&lc.slot[b], &lc.cap_slot[b], nwords, 8);
-                if (rccl)
-                    KH_NCCL(ncclBroadcast(lc.slot[b], lc.slot[b], nwords, ncclUint64, s, G->comm_b, lc.st_x));
-                else
-                    KH_HIP(hipMemcpyAsync(lc.slot[b], d_words[s], nwords * 8, hipMemcpyDeviceToDevice, lc.st_x));
+                KH_HIP(hipMemcpyAsync(lc.slot[b], R.d[s], nunits * esz, hipMemcpyDeviceToDevice, lc.st_x));
             }
             KH_HIP(hipEventRecord(lc.ev_ready[b], lc.st_x));
         }
@@ -2732,29 +2966,23 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
     transfer(0);
     for (int s = 0; s < W; s++) {
         if (s + 1 < W) transfer(s + 1);
-        std::vector<const uint64_t *> buf(NL);
+        std::vector<const void *> buf(NL);
         for (int l = 0; l < NL; l++) {
             auto &lc = G->loc[l];
             KH_HIP(hipSetDevice(G->shards[l]->device));
             KH_HIP(hipStreamWaitEvent(G->shards[l]->stream, lc.ev_ready[s & 1], 0));
-            buf[l] = own(s, l) ? d_words[0] : lc.slot[s & 1];
+            buf[l] = own(s, l) ? R.d[0] : (const void *)lc.slot[s & 1];
         }
         for (uint64_t r0 = 0; r0 < nreads; r0 += rpb) {
             const uint64_t nr = std::min(rpb, nreads - r0);
             std::vector<PassState> ps(NL);
-            std::vector<SrcTwoBit> srcs(NL);
-            for (int l = 0; l < NL; l++) {
+            std::vector<Src> srcs(NL);
+            GROUP_TRY(for (int l = 0; l < NL; l++) {
                 Graph *g = G->shards[l];
                 KH_HIP(hipSetDevice(g->device));
-                SrcTwoBit sb = src_twobit(g, buf[l]);
-                set_fixed(sb, kpr);
-                sb.koff = nullptr;
-                sb.nreads = nr;
-                sb.kbase = r0 * kpr;
-                sb.rbase = 0;
-                srcs[l] = sb;
-                ps[l] = pass_stage_a(g, sb, nr * kpr);
-            }
+                srcs[l] = group_src<Src>(g, R, buf[l], r0, nr);
+                ps[l] = pass_stage_a(g, srcs[l], nr * kpr);
+            });
             if (r0 == 0 && s + 1 < W) {
                 // No comm_b broadcast is ever in flight together with an
                 // operation on G->comm: broadcast s+1 starts after source
@@ -2769,10 +2997,10 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
             }
             group_route_winners(G, ps);
             if (ps[0].bigc) group_merge_full(G, ps);
-            for (int l = 0; l < NL; l++) {
+            GROUP_TRY(for (int l = 0; l < NL; l++) {
                 KH_HIP(hipSetDevice(G->shards[l]->device));
                 pass_stage_c(G->shards[l], srcs[l], ps[l], nullptr);
-            }
+            });
         }
         for (int l = 0; l < NL; l++) {
             auto &lc = G->loc[l];
@@ -2786,6 +3014,301 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
         KH_HIP(hipStreamSynchronize(G->loc[l].st_x));
         KH_HIP(hipStreamSynchronize(G->shards[l]->stream));   // the slots are free for the next call
     }
+}
+
+// every rank must pass the same shape (the collective schedule depends on it)
+static void group_check_shape(ShardGroup *G, uint64_t nreads, uint64_t read_len) {
+    if (!per_rank(G)) return;
+    Graph *g0 = G->shards[0];
+    uint64_t h[2] = {nreads, read_len};
+    KH_HIP(hipSetDevice(g0->device));
+    KH_HIP(hipMemcpyAsync(G->d_red + 140, h, 16, hipMemcpyHostToDevice, g0->stream));
+    coll_allreduce_u64(G, g0->stream, G->d_red + 140, G->d_red + 142, 2, RED_MAX);
+    coll_allreduce_u64(G, g0->stream, G->d_red + 140, G->d_red + 144, 2, RED_MIN);
+    uint64_t mm[4];
+    KH_HIP(hipMemcpyAsync(mm, G->d_red + 142, 32, hipMemcpyDeviceToHost, g0->stream));
+    KH_HIP(hipStreamSynchronize(g0->stream));
+    if (mm[0] != mm[2] || mm[1] != mm[3]) fail(KH_EVALUE, "ranks passed different read counts or lengths");
+}
+
+static GroupReads group_reads(ShardGroup *G, bool bytes, const void *const *d, uint64_t nreads, uint64_t read_len) {
+    Graph *g0 = G->shards[0];
+    if (bytes && g0->hash != MURMUR) fail(KH_EVALUE, "ASCII reads are for Murmur-hashed (Counttable) groups");
+    if (!bytes && g0->hash != TWOBIT) fail(KH_EVALUE, "packed 2-bit reads are for 2-bit hashed groups");
+    if (read_len < (uint64_t)g0->k) fail(KH_EVALUE, "reads shorter than k");
+    group_check_shape(G, nreads, read_len);
+    GroupReads R;
+    R.bytes = bytes;
+    R.d = d;
+    R.nreads = nreads;
+    R.read_len = read_len;
+    R.kpr = read_len - g0->k + 1;
+    return R;
+}
+
+// collective: every rank passes its own fixed-length packed reads (same
+// count and length on every rank); consumed as the stream rank 0, 1, ...
+// (exchange mode: pass-interleaved, see group_consume_a2a)
+void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len) {
+    const GroupReads R = group_reads(G, false, (const void *const *)d_words, nreads, read_len);
+    if (!nreads) return;
+    if (G->a2a) group_consume_a2a<SrcTwoBit>(G, R);
+    else group_consume_bcast<SrcTwoBit>(G, R);
+}
+
+// the same for ASCII reads of a Murmur-hashed (Counttable family) group
+void group_consume_bytes_fixed(ShardGroup *G, const uint8_t *const *d_bytes, uint64_t nreads, uint64_t read_len) {
+    const GroupReads R = group_reads(G, true, (const void *const *)d_bytes, nreads, read_len);
+    if (!nreads) return;
+    if (G->a2a) group_consume_a2a<SrcBytes>(G, R);
+    else group_consume_bcast<SrcBytes>(G, R);
+}
+
+// ---------------------------------------------------------------------------
+// Sharded get_median_count (Hashtable::get_median_count,
+// src/oxli/hashtable.cc:299-328) of every rank's own fixed-length reads.  A
+// k-mer's N bins live on different ranks, so its count -- the minimum over
+// the tables, then the bigcount value when a Byte minimum is 255
+// (storage.hh:627-649) -- is assembled from the owners:
+//   exchange mode: the k-mers are partitioned into the unsharded level-1
+//     buckets exactly as in a consume pass (a2a_level1) and every bucket
+//     range goes to its owner (a2a_exchange); the owner reads each routed
+//     record's table value and keeps the per-k-mer minimum in a u8 array over
+//     the pass's k-mer index space (k_lookup_min); a MIN reduce-scatter over
+//     ranks leaves every rank the minima of its own k-mers.
+//   broadcast mode: every source's reads are broadcast, every rank takes the
+//     minimum over the tables whose bin it owns (k_own_min), and a MIN reduce
+//     to the source rank completes them.
+// The read's home rank then computes median / average / stddev from the
+// minima (k_median_fixed with cnt8; bigcount map replicated on every rank).
+struct QueryOut {
+    uint16_t *const *med;
+    float *const *avg;
+    float *const *sd;
+};
+
+template <class Src>
+static void group_median_reads(Graph *g, const GroupReads &R, const void *buf, uint64_t r0, uint64_t nr,
+                               const uint8_t *cnt8, uint16_t *med, float *avg, float *sd) {
+    const Src src = group_src<Src>(g, R, buf, r0, nr);
+    const unsigned grid = (unsigned)std::min<uint64_t>((nr + 3) / 4, 8192);
+    TIMED("median", hipLaunchKernelGGL(k_median_fixed<Src>, dim3(grid), dim3(256), 0, g->stream, g->prm, src, nr,
+                                       (uint32_t)R.kpr, g->d_tab, g->d_bc_keys, g->d_bc_vals, g->d_bc_n, med + r0,
+                                       avg + r0, sd + r0, cnt8));
+    KH_HIP(hipGetLastError());
+}
+
+template <class Src>
+static void group_median_a2a(ShardGroup *G, const GroupReads &R, const QueryOut &Q) {
+    const int W = G->world, NL = G->nlocal;
+    Graph *g0 = G->shards[0];
+    uint64_t rpb, stride;
+    a2a_pass_plan(G, g0, R, &rpb, &stride);
+    const uint64_t nk = (uint64_t)W * stride;
+    constexpr uint32_t PARTS = 4;   // workgroups per (source, bucket) segment
+    for (uint64_t r0 = 0; r0 < R.nreads; r0 += rpb) {
+        const uint64_t nr = std::min(rpb, R.nreads - r0), nkc = nr * R.kpr;
+        GROUP_TRY(for (int l = 0; l < NL; l++) {
+            Graph *V = G->views[l];
+            KH_HIP(hipSetDevice(V->device));
+            V->use_bigcount = false;
+            a2a_level1(V, group_src<Src>(V, R, R.d[l], r0, nr), nkc, (uint32_t)((uint64_t)(G->rank0 + l) * stride));
+        });
+        std::vector<uint64_t> meta;
+        a2a_meta(G, meta);
+        const uint64_t F1v = G->views[0]->prm.F1, M = 2 * (F1v + 1);
+        GROUP_TRY(for (int l = 0; l < NL; l++) {
+            const int r = G->rank0 + l;
+            Graph *g = G->shards[l];
+            auto &lc = G->loc[l];
+            KH_HIP(hipSetDevice(g->device));
+            uint64_t need = 0;
+            for (int s = 0; s < W; s++) need += meta[(size_t)s * M + G->B[r + 1]] - meta[(size_t)s * M + G->B[r]];
+            ensure_recs(g, need);
+            ensure((void **)&lc.q8, &lc.cap_q8, nk + 64, 1);
+            ensure((void **)&lc.o8, &lc.cap_o8, std::max<uint64_t>(stride, nk) + 64, 1);
+        });
+        std::vector<std::vector<uint64_t>> rb;
+        a2a_exchange(G, meta, rb);
+        GROUP_TRY(for (int l = 0; l < NL; l++) {
+            const int r = G->rank0 + l;
+            Graph *g = G->shards[l];
+            auto &lc = G->loc[l];
+            KH_HIP(hipSetDevice(g->device));
+            const uint64_t nseg = a2a_segments(G, l, meta, rb[l]);
+            KH_HIP(hipMemsetAsync(lc.q8, 0xFF, (nk + 3) & ~3ull, g->stream));
+            if (nseg)
+                TIMED("lookup", hipLaunchKernelGGL(k_lookup_min, dim3((unsigned)(nseg * PARTS)), dim3(256), 0,
+                                                   g->stream, g->prm, g->d_tab, g->ws.rec1, lc.seg,
+                                                   lc.seg + nseg + 1, G->B[r + 1] - G->B[r], PARTS,
+                                                   (uint32_t *)lc.q8));
+            KH_HIP(hipGetLastError());
+        });
+        // MIN reduce-scatter: rank r's minima = min over ranks of chunk r
+        if (G->comm) {
+            Graph *g = G->shards[0];
+            auto &lc = G->loc[0];
+            KH_NCCL(ncclReduceScatter(lc.q8, lc.o8, stride, ncclUint8, ncclMin, G->comm, g->stream));
+        } else if (G->hosted) {
+            Graph *g = G->shards[0];
+            auto &lc = G->loc[0];
+            std::vector<uint8_t> hs(nk), hr(nk);
+            std::vector<uint64_t> sb(W, stride), rbb(W, stride);
+            KH_HIP(hipMemcpyAsync(hs.data(), lc.q8, nk, hipMemcpyDeviceToHost, g->stream));
+            KH_HIP(hipStreamSynchronize(g->stream));
+            host_rc(G->tp.alltoallv(G->tp.ctx, hs.data(), sb.data(), hr.data(), rbb.data()), "alltoallv");
+            KH_HIP(hipMemcpyAsync(lc.q8, hr.data(), nk, hipMemcpyHostToDevice, g->stream));
+            KH_HIP(hipMemsetAsync(lc.o8, 0xFF, stride, g->stream));
+            hipLaunchKernelGGL(k_min_bytes, dim3((unsigned)std::min<uint64_t>((stride + 255) / 256, 8192)), dim3(256),
+                               0, g->stream, lc.o8, lc.q8, stride, W, stride);
+        } else {
+            for (int l = 0; l < NL; l++) KH_HIP(hipStreamSynchronize(G->shards[l]->stream));
+            for (int l = 0; l < NL; l++) {
+                Graph *g = G->shards[l];
+                auto &lc = G->loc[l];
+                KH_HIP(hipMemsetAsync(lc.o8, 0xFF, stride, g->stream));
+                for (int s = 0; s < W; s++)
+                    hipLaunchKernelGGL(k_min_bytes, dim3((unsigned)std::min<uint64_t>((stride + 255) / 256, 8192)),
+                                       dim3(256), 0, g->stream, lc.o8, G->loc[s].q8 + (uint64_t)l * stride, 0, 1,
+                                       stride);
+            }
+            for (int l = 0; l < NL; l++) KH_HIP(hipStreamSynchronize(G->shards[l]->stream));
+        }
+        KH_HIP(hipGetLastError());
+        GROUP_TRY(for (int l = 0; l < NL; l++) {
+            Graph *g = G->shards[l];
+            KH_HIP(hipSetDevice(g->device));
+            group_median_reads<Src>(g, R, R.d[l], r0, nr, G->loc[l].o8, Q.med[l], Q.avg[l], Q.sd[l]);
+            (void)nkc;
+        });
+    }
+}
+
+template <class Src>
+static void group_median_bcast(ShardGroup *G, const GroupReads &R, const QueryOut &Q) {
+    const int W = G->world, NL = G->nlocal;
+    Graph *g0 = G->shards[0];
+    const uint64_t nunits = R.units();
+    const size_t esz = R.esize();
+    const uint64_t slot_words = (nunits * esz + 64 + 7) / 8;
+    const uint64_t rpb0 = std::max<uint64_t>(1, std::min<uint64_t>(g0->batch_kmers, MAX_PASS_KMERS) / R.kpr);
+    const uint64_t npass = std::max<uint64_t>(1, (R.nreads + rpb0 - 1) / rpb0);
+    const uint64_t rpb = std::max<uint64_t>(1, (R.nreads + npass - 1) / npass);
+    auto own = [&](int s, int l) { return per_rank(G) && G->rank0 + l == s; };
+    for (int s = 0; s < W; s++) {
+        // source s's reads on every local shard (loopback: read in place)
+        std::vector<const void *> buf(NL);
+        for (int l = 0; l < NL; l++) {
+            Graph *g = G->shards[l];
+            auto &lc = G->loc[l];
+            KH_HIP(hipSetDevice(g->device));
+            if (!per_rank(G)) {
+                buf[l] = R.d[s];
+                continue;
+            }
+            if (!own(s, l)) {
+                ensure((void **)&lc.slot[0], &lc.cap_slot[0], slot_words, 8);
+                KH_HIP(hipMemsetAsync((uint8_t *)lc.slot[0] + nunits * esz, 0, 64, g->stream));
+            }
+            void *dst = own(s, l) ? const_cast<void *>(R.d[0]) : (void *)lc.slot[0];
+            if (G->comm) {
+                KH_NCCL(ncclBroadcast(dst, dst, nunits, R.nccl_type(), s, G->comm_b, g->stream));
+            } else {
+                std::vector<uint8_t> hb(nunits * esz);
+                KH_HIP(hipStreamSynchronize(g->stream));
+                if (own(s, l)) KH_HIP(hipMemcpy(hb.data(), R.d[0], hb.size(), hipMemcpyDeviceToHost));
+                host_rc(G->tp.broadcast(G->tp.ctx, hb.data(), hb.size(), s), "broadcast");
+                if (!own(s, l)) KH_HIP(hipMemcpy(dst, hb.data(), hb.size(), hipMemcpyHostToDevice));
+            }
+            buf[l] = dst;
+        }
+        for (uint64_t r0 = 0; r0 < R.nreads; r0 += rpb) {
+            const uint64_t nr = std::min(rpb, R.nreads - r0), nk = nr * R.kpr;
+            GROUP_TRY(for (int l = 0; l < NL; l++) {
+                Graph *g = G->shards[l];
+                auto &lc = G->loc[l];
+                KH_HIP(hipSetDevice(g->device));
+                ensure((void **)&lc.q8, &lc.cap_q8, nk + 64, 1);
+                const Src src = group_src<Src>(g, R, buf[l], r0, nr);
+                const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nk + 255) / 256, 16384));
+                TIMED("own_min", hipLaunchKernelGGL(k_own_min<Src>, dim3(grid), dim3(256), 0, g->stream, g->prm, src,
+                                                    nk, g->d_tab, lc.q8));
+                KH_HIP(hipGetLastError());
+            });
+            // MIN reduce to the source rank
+            int root_l = -1;
+            if (G->comm) {
+                Graph *g = G->shards[0];
+                auto &lc = G->loc[0];
+                KH_NCCL(ncclReduce(lc.q8, lc.q8, nk, ncclUint8, ncclMin, s, G->comm, g->stream));
+                if (own(s, 0)) root_l = 0;
+            } else if (G->hosted) {
+                Graph *g = G->shards[0];
+                auto &lc = G->loc[0];
+                std::vector<uint8_t> mine(nk), all((size_t)W * nk);
+                KH_HIP(hipMemcpyAsync(mine.data(), lc.q8, nk, hipMemcpyDeviceToHost, g->stream));
+                KH_HIP(hipStreamSynchronize(g->stream));
+                host_rc(G->tp.allgather(G->tp.ctx, mine.data(), all.data(), nk), "allgather");
+                if (own(s, 0)) {
+                    for (uint64_t q = 0; q < nk; q++) {
+                        uint8_t c = 0xFF;
+                        for (int t = 0; t < W; t++) c = std::min(c, all[(size_t)t * nk + q]);
+                        mine[q] = c;
+                    }
+                    KH_HIP(hipMemcpyAsync(lc.q8, mine.data(), nk, hipMemcpyHostToDevice, g->stream));
+                    KH_HIP(hipStreamSynchronize(g->stream));
+                    root_l = 0;
+                }
+            } else {
+                for (int l = 0; l < NL; l++) KH_HIP(hipStreamSynchronize(G->shards[l]->stream));
+                Graph *g = G->shards[s];
+                for (int t = 0; t < W; t++)
+                    if (t != s)
+                        hipLaunchKernelGGL(k_min_bytes, dim3((unsigned)std::min<uint64_t>((nk + 255) / 256, 8192)),
+                                           dim3(256), 0, g->stream, G->loc[s].q8, G->loc[t].q8, 0, 1, nk);
+                root_l = s;
+            }
+            KH_HIP(hipGetLastError());
+            if (root_l >= 0) {
+                Graph *g = G->shards[root_l];
+                KH_HIP(hipSetDevice(g->device));
+                group_median_reads<Src>(g, R, buf[root_l], r0, nr, G->loc[root_l].q8, Q.med[root_l], Q.avg[root_l],
+                                        Q.sd[root_l]);
+            }
+            // the next pass reuses every shard's q8
+            for (int l = 0; l < NL; l++) KH_HIP(hipStreamSynchronize(G->shards[l]->stream));
+        }
+    }
+}
+
+// collective: d_reads[l] = local shard l's own fixed-length reads (packed
+// 2-bit words, or ASCII bytes for Murmur groups); its outputs go to
+// d_med[l] / d_avg[l] / d_sd[l] (device, one entry per read)
+void group_median_fixed(ShardGroup *G, const void *const *d_reads, uint64_t nreads, uint64_t read_len,
+                        uint16_t *const *d_med, float *const *d_avg, float *const *d_sd) {
+    Graph *g0 = G->shards[0];
+    const bool bytes = g0->hash == MURMUR;
+    const GroupReads R = group_reads(G, bytes, d_reads, nreads, read_len);
+    if (R.kpr > 256) fail(KH_EVALUE, "device median path takes at most 256 k-mers per read");
+    if (!nreads) return;
+    for (Graph *g : G->shards) {
+        KH_HIP(hipSetDevice(g->device));
+        engine_sync_bigcounts(g);
+    }
+    const QueryOut Q{d_med, d_avg, d_sd};
+    if (G->a2a) {
+        if (bytes) group_median_a2a<SrcBytes>(G, R, Q);
+        else group_median_a2a<SrcTwoBit>(G, R, Q);
+    } else {
+        if (bytes) group_median_bcast<SrcBytes>(G, R, Q);
+        else group_median_bcast<SrcTwoBit>(G, R, Q);
+    }
+    for (Graph *g : G->shards) {
+        KH_HIP(hipSetDevice(g->device));
+        KH_HIP(hipStreamSynchronize(g->stream));
+        engine_collect_events(g);
+    }
+    for (Graph *V : G->views) KH_HIP(hipStreamSynchronize(V->stream));
 }
 
 // n_unique / n_occupied of the whole group (collective in RCCL mode)

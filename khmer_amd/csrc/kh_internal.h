@@ -69,12 +69,22 @@ struct Geometry {
 };
 
 // kernel parameter block (passed by value)
+// Timing-only ablations (bench.py --ablate, tools/lb_ablate.sh): switches that
+// skip work and give wrong tables.  They exist only in a development build
+// compiled with -DKH_ABLATE (make EXTRA_HIPFLAGS=-DKH_ABLATE); in the product
+// library KH_ABL is constant false and the KH_ABLATE variable is ignored.
+#ifdef KH_ABLATE
+#define KH_ABL(P, bit) ((P).ablate & (bit))
+#else
+#define KH_ABL(P, bit) 0
+#endif
+
 struct Params {
     int kind, hash, k, n;
     int s0, s2;
     uint32_t F1;
     int use_bigcount;
-    int ablate;               // timing-only ablation bits (KH_ABLATE env); 0 in normal use
+    int ablate;               // timing-only ablation bits (KH_ABLATE env, -DKH_ABLATE builds only)
     uint64_t p[MAXT];         // table sizes (bins) -- the primes the hash is reduced by
     uint64_t lo[MAXT];        // first bin of table i held here (0 unless sharded)
     uint64_t lsz[MAXT];       // bins of table i held here (p[i] unless sharded)
@@ -125,6 +135,7 @@ struct Workspace {
     // fixed-capacity level 1 (k_scatter_l1f): bucket b holds [bkt_base[b], bkt_cur[b])
     uint64_t *bkt_base = nullptr, *bkt_cur = nullptr;
     uint64_t bkt_nkmers = 0, bkt_total = 0;
+    bool l1_exact = false;           // exchange-mode view: level 1 took the exact path (buckets = off1)
     uint64_t *ctr = nullptr;         // counters, see CTR_*
     uint64_t *h_ctr = nullptr;       // pinned host mirror
     uint64_t cap_regions = 0, cap_xseg = 0;
@@ -294,6 +305,9 @@ int group_exchange(ShardGroup *G);
 void group_comm_info(ShardGroup *G, int *nranks, int *device);
 void group_destroy(ShardGroup *G);
 void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len);
+void group_consume_bytes_fixed(ShardGroup *G, const uint8_t *const *d_bytes, uint64_t nreads, uint64_t read_len);
+void group_median_fixed(ShardGroup *G, const void *const *d_reads, uint64_t nreads, uint64_t read_len,
+                        uint16_t *const *d_med, float *const *d_avg, float *const *d_sd);
 void group_counters(ShardGroup *G, uint64_t *n_unique, uint64_t *n_occupied);
 int group_world(ShardGroup *G);
 int group_nlocal(ShardGroup *G);

@@ -213,11 +213,26 @@ __global__ void k_at_least(const uint64_t *koff, uint64_t nreads, const uint16_t
 // exact integer sum; the squared deviations are summed in stream order by a
 // uniform loop (the same rounding sequence as the reference); median =
 // sorted[kpr / 2] by a radix select over the counts with wave ballots.
+//
+// cnt8 != null (a sharded group's query, kh_engine.hip group_median_fixed):
+// the k-mer counts are the per-k-mer minima over the tables gathered from the
+// shards that own the bins (u8: tables are at most 8-bit), and a Byte count
+// of 255 becomes the bigcount value from the replicated map, as
+// ByteStorage::get_count does (storage.hh:627-649).
+__device__ __forceinline__ uint32_t bigcount_or(uint64_t h, uint32_t c, const uint64_t *bc_keys,
+                                                const uint16_t *bc_vals, uint64_t bc_n) {
+    uint64_t lo = 0, hi = bc_n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (bc_keys[mid] < h) lo = mid + 1; else hi = mid;
+    }
+    return lo < bc_n && bc_keys[lo] == h ? bc_vals[lo] : c;
+}
 template <class Src>
 __global__ void __launch_bounds__(256) k_median_fixed(Params P, Src src, uint64_t nreads, uint32_t kpr,
                                                       const uint8_t *tab, const uint64_t *bc_keys,
                                                       const uint16_t *bc_vals, uint64_t bc_n, uint16_t *med,
-                                                      float *avg, float *sd) {
+                                                      float *avg, float *sd, const uint8_t *cnt8 = nullptr) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -229,7 +244,15 @@ __global__ void __launch_bounds__(256) k_median_fixed(Params P, Src src, uint64_
         for (int s = 0; s < 4; s++) {
             const uint32_t t = lane + 64u * s;
             ok[s] = t < kpr;
-            c[s] = ok[s] ? get_count_dev(P, tab, kmer_hash_global(src, r * kpr + t), bc_keys, bc_vals, bc_n) : 0;
+            if (!ok[s]) {
+                c[s] = 0;
+            } else if (cnt8) {
+                c[s] = cnt8[r * kpr + t];
+                if (c[s] == 255 && P.kind == BYTE && P.use_bigcount && bc_n)
+                    c[s] = bigcount_or(kmer_hash_global(src, r * kpr + t), c[s], bc_keys, bc_vals, bc_n);
+            } else {
+                c[s] = get_count_dev(P, tab, kmer_hash_global(src, r * kpr + t), bc_keys, bc_vals, bc_n);
+            }
             sum += c[s];
             mx = c[s] > mx ? c[s] : mx;
         }
@@ -274,6 +297,92 @@ __global__ void __launch_bounds__(256) k_median_fixed(Params P, Src src, uint64_
             avg[r] = average;
             sd[r] = var;
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Sharded get_median_count (kh_engine.hip group_median_fixed): the minimum
+// over the tables of every k-mer, gathered from the shards owning its bins.
+
+// table value of local bin `bin` of table i (Storage::get_count's per-table
+// read, storage.hh:206-219, 362-379, 627-649; a shard's slice starts on a
+// multiple of 8 bins, so the nibble parity and bit position are the global ones)
+__device__ __forceinline__ uint32_t table_value(const Params &P, const uint8_t *tab, int i, uint64_t bin) {
+    if (P.kind == BIT) return (tab[P.tbyte[i] + (bin >> 3)] >> (bin & 7)) & 1;
+    if (P.kind == NIBBLE) {
+        const uint8_t byte = tab[P.tbyte[i] + (bin >> 1)];
+        return (bin & 1) ? (byte & 0x0F) : (byte >> 4);
+    }
+    return tab[P.tbyte[i] + bin];
+}
+
+// res[j] = min(res[j], c) on a byte array through CAS on its 32-bit word
+__device__ __forceinline__ void atomic_min_u8(uint32_t *res32, uint64_t j, uint32_t c) {
+    uint32_t *p = res32 + (j >> 2);
+    const int sh = (int)(j & 3) * 8;
+    uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (((cur >> sh) & 0xFFu) > c) {
+        const uint32_t nw = (cur & ~(0xFFu << sh)) | (c << sh);
+        const uint32_t prev = atomicCAS(p, cur, nw);
+        if (prev == cur) break;
+        cur = prev;
+    }
+}
+
+// Exchange mode: the owner looks up the level-1 records routed to it.
+// Segment x = s * NB + b holds source s's records of the owner's bucket b:
+// (j << 32) | offset inside the bucket's 2^(s0+s2) bins (sentinel ~0 in
+// partially filled blocks).  `parts` workgroups per segment.
+__global__ void k_lookup_min(Params P, const uint8_t *tab, const uint64_t *rec, const uint64_t *seg_lo,
+                             const uint64_t *seg_hi, uint32_t NB, uint32_t parts, uint32_t *res32) {
+    const uint64_t x = blockIdx.x / parts, part = blockIdx.x % parts;
+    const uint64_t lo = seg_lo[x], hi = seg_hi[x];
+    const uint32_t b = (uint32_t)(x % NB);
+    const int shift = P.s0 + P.s2;
+    // the bucket's table (tables start on bucket boundaries)
+    int ti = 0;
+    const uint64_t g0 = (uint64_t)b << shift;
+    while (ti + 1 < P.n && g0 >= P.tbase[ti + 1]) ti++;
+    const uint64_t base = g0 - P.tbase[ti];
+    const uint64_t n = hi > lo ? hi - lo : 0, per = (n + parts - 1) / parts;
+    const uint64_t a0 = lo + part * per, a1 = min(hi, a0 + per);
+    for (uint64_t a = a0 + threadIdx.x; a < a1; a += blockDim.x) {
+        const uint64_t v = rec[a];
+        if (v == ~0ull) continue;
+        const uint64_t bin = base + (v & ((1ull << shift) - 1));
+        atomic_min_u8(res32, v >> 32, table_value(P, tab, ti, bin));
+    }
+}
+
+// Broadcast mode: every rank hashes every k-mer of a source's reads and
+// takes the minimum over the tables whose bin it owns (0xFF: none)
+template <class Src>
+__global__ void __launch_bounds__(256) k_own_min(Params P, Src src, uint64_t nkmers, const uint8_t *tab,
+                                                 uint8_t *out) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < nkmers;
+         j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t h = kmer_hash_global(src, j);
+        uint32_t c = 0xFF;
+        for (int i = 0; i < P.n; i++) {
+            const uint64_t bin = mod_barrett(h, P.p[i], P.m[i]) - P.lo[i];
+            if (bin < P.lsz[i]) {
+                const uint32_t v = table_value(P, tab, i, bin);
+                c = v < c ? v : c;
+            }
+        }
+        out[j] = (uint8_t)c;
+    }
+}
+
+// dst[q] = min over the `nsrc` arrays src + t * stride (bytes), q < n
+__global__ void k_min_bytes(uint8_t *dst, const uint8_t *src, uint64_t stride, int nsrc, uint64_t n) {
+    for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < n; q += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t c = dst[q];
+        for (int t = 0; t < nsrc; t++) {
+            const uint32_t v = src[(uint64_t)t * stride + q];
+            c = v < c ? v : c;
+        }
+        dst[q] = (uint8_t)c;
     }
 }
 

@@ -27,7 +27,10 @@ import ctypes
 from . import _lib
 from ._lib import lib, check
 
-KIND = {"Countgraph": _lib.STORAGE_BYTE, "Nodegraph": _lib.STORAGE_BIT, "SmallCountgraph": _lib.STORAGE_NIBBLE}
+KIND = {"Countgraph": _lib.STORAGE_BYTE, "Nodegraph": _lib.STORAGE_BIT, "SmallCountgraph": _lib.STORAGE_NIBBLE,
+        # the Counttable family: MurmurHash3 over ASCII k-mers (include/oxli/hashtable.hh:494-627)
+        "Counttable": _lib.STORAGE_BYTE, "Nodetable": _lib.STORAGE_BIT, "SmallCounttable": _lib.STORAGE_NIBBLE}
+MURMUR_CLASSES = {"Counttable", "Nodetable", "SmallCounttable"}
 
 
 def shard_lo(p, world, r):
@@ -209,6 +212,8 @@ class ShardedGraph(object):
         self._h = None
         self.shards = []
         self.kind = KIND[cls]
+        self.murmur = cls in MURMUR_CLASSES
+        hash_kind = _lib.HASH_MURMUR if self.murmur else _lib.HASH_TWOBIT
         self.k, self.sizes, self.world = k, [int(x) for x in sizes], world
         self.loopback = loopback
         self.transport = transport
@@ -219,10 +224,10 @@ class ShardedGraph(object):
         mode = _lib.GROUP_EXCHANGE if exchange else _lib.GROUP_BROADCAST
         self.exchange = bool(exchange)
         if transport is not None:
-            check(lib.kh_group_create_hosted_mode(self.kind, _lib.HASH_TWOBIT, k, arr, len(sizes), world, rank,
+            check(lib.kh_group_create_hosted_mode(self.kind, hash_kind, k, arr, len(sizes), world, rank,
                                                   device, ctypes.byref(transport.struct), mode, ctypes.byref(h)))
         else:
-            check(lib.kh_group_create_mode(self.kind, _lib.HASH_TWOBIT, k, arr, len(sizes), world, rank, nlocal,
+            check(lib.kh_group_create_mode(self.kind, hash_kind, k, arr, len(sizes), world, rank, nlocal,
                                            devs, uid, mode, ctypes.byref(h)))
         self._h = h
         w, nl, r0 = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
@@ -291,6 +296,23 @@ class ShardedGraph(object):
                                                    for p in d_words])
         check(lib.kh_group_consume_packed_fixed_device(self._h, ptrs, int(nreads), int(read_len)))
 
+    @staticmethod
+    def _ptrs(ps):
+        return (ctypes.c_void_p * len(ps))(*[int(p) if not isinstance(p, ctypes.c_void_p) else p.value for p in ps])
+
+    def consume_bytes_fixed_device(self, d_bytes, nreads, read_len):
+        """Collective (Counttable family): d_bytes = one device pointer per
+        local shard to its own ASCII fixed-length reads."""
+        check(lib.kh_group_consume_bytes_fixed_device(self._h, self._ptrs(d_bytes), int(nreads), int(read_len)))
+
+    def median_fixed_device(self, d_reads, nreads, read_len, d_med, d_avg, d_sd):
+        """Collective get_median_count (src/oxli/hashtable.cc:299-328) of every
+        rank's own fixed-length reads (packed words, or ASCII bytes for the
+        Counttable family); outputs into the device arrays d_med / d_avg /
+        d_sd (one pointer per local shard, one entry per read)."""
+        check(lib.kh_group_median_fixed_device(self._h, self._ptrs(d_reads), int(nreads), int(read_len),
+                                               self._ptrs(d_med), self._ptrs(d_avg), self._ptrs(d_sd)))
+
     def counters(self):
         """(n_unique_kmers, n_occupied) of the whole group (collective)."""
         u, o = ctypes.c_uint64(), ctypes.c_uint64()
@@ -305,7 +327,7 @@ class ShardedGraph(object):
         """Reference-layout table bytes of the whole group.  Loopback: from the
         local shards; one process per rank: every rank's slices through the
         rendezvous `rdv` (khmer_amd.rendezvous.Rendezvous)."""
-        if self.loopback:
+        if self.loopback or self.world == 1:
             parts = self.local_tables()
         else:
             mine = self.local_tables()[0]

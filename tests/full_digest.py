@@ -32,7 +32,48 @@ CONFIGS = {
     # skewed ("genomic") stream, 2 Mbp genome at ~750x: saturation + heavy bigcount
     "genomic_c2": dict(kind=1, hash=0, k=21, n=4, x=1e9, reads=10_000_000, L=150, bigcount=True,
                        genome=2_000_000, batch_kmers=1 << 29),
+    # C5 query geometry with counts that spread over 1..15 and saturate (VERDICT
+    # r3 "Next round" #3): 4 x 8e9 nibbles, genomic streams at ~8x k-mer coverage
+    "c5_genomic": dict(kind=7, hash=0, k=31, n=4, x=8e9, reads=4_000_000, L=150, bigcount=False,
+                       genome=50_000_000, batch_kmers=1 << 27),
+    "c5m_genomic": dict(kind=7, hash=1, k=51, n=4, x=8e9, reads=1_000_000, L=150, bigcount=False,
+                        genome=10_000_000, batch_kmers=1 << 26),
 }
+
+# Exchange-mode (Option A) streams: a `world`-rank group consumes reads
+# [s * reads / world, (s + 1) * reads / world) on rank s in passes that take
+# the next chunk of every rank in rank order (khmer_amd.parallel.exchange_passes
+# at `batch_kmers`); n_unique and the bigcount map follow that order.
+EXCHANGE = {
+    "c2_full_x2": ("c2_full", 2, 1600 << 20),      # tests/test_gpu_shard.py loopback
+    "c2_full_x8": ("c2_full", 8, 1600 << 20),
+    "c2_full_x2b": ("c2_full", 2, 3200 << 20),     # bench.py --gpus 2 --strong (default batch)
+    "genomic_c2_x2": ("genomic_c2", 2, 1 << 29),
+    "c4_shape_x2": ("c4_shape", 2, 1 << 28),
+    "c4_shape_x8": ("c4_shape", 8, 1 << 28),
+    "c5m_shape_x2": ("c5m_shape", 2, 1 << 26),
+    "c5m_shape_x8": ("c5m_shape", 8, 1 << 26),
+    "c5m_genomic_x2": ("c5m_genomic", 2, 1 << 26),
+    "c5m_genomic_x8": ("c5m_genomic", 8, 1 << 26),
+}
+for _name, (_base, _world, _batch) in EXCHANGE.items():
+    CONFIGS[_name] = dict(CONFIGS[_base], exchange=[_world, _batch])
+
+
+def stream_chunks(c, step=1_000_000):
+    """[(r0, nreads)] in the order the configuration's stream consumes them:
+    the reads in order, or the exchange-mode pass interleave."""
+    if "exchange" not in c:
+        return [(r0, min(step, c["reads"] - r0)) for r0 in range(0, c["reads"], step)]
+    from khmer_amd.parallel import exchange_passes
+    world, batch = c["exchange"]
+    per = c["reads"] // world
+    out = []
+    for r0, nr in exchange_passes(per, c["L"], c["k"], world, batch):
+        for s in range(world):
+            for a in range(0, nr, step):
+                out.append((s * per + r0 + a, min(step, nr - a)))
+    return out
 
 
 def sha256_view(mv, chunk=1 << 28):
@@ -62,7 +103,7 @@ def median_digest(med, avg, sd):
 
 # get_median_count digests over the first MEDIAN_READS reads of the stream,
 # for the configurations whose query path the bench measures (C5 / C5M)
-MEDIAN_READS = {"c5_shape": 1_000_000, "c5m_shape": 1_000_000}
+MEDIAN_READS = {"c5_shape": 1_000_000, "c5m_shape": 1_000_000, "c5_genomic": 1_000_000, "c5m_genomic": 1_000_000}
 
 
 def fixture_path(name):

@@ -28,9 +28,8 @@ def make(name):
     t.set_use_bigcount(c["bigcount"])
     t0 = time.time()
     kmers = 0
-    step = 1_000_000
-    for r0 in range(0, c["reads"], step):
-        kmers += t.consume_synth(synth.SEED, r0, min(step, c["reads"] - r0), c["L"], genome=c["genome"])
+    for r0, nr in FD.stream_chunks(c):
+        kmers += t.consume_synth(synth.SEED, r0, nr, c["L"], genome=c["genome"])
     secs = time.time() - t0
     nbc, bcd = FD.bigcount_digest(t.bigcounts())
     out = {
@@ -47,6 +46,8 @@ def make(name):
         out["median_reads"] = nmed
         out["median_sha256"] = FD.median_digest(med, avg, sd)
         out["median_max"] = int(med.max())
+        import numpy as np
+        out["median_hist"] = np.bincount(med.astype(np.int64), minlength=16)[:16].tolist()
         out["generator"] += ", median digest %.0f s" % (time.time() - t0)
     os.makedirs(FD.FULL, exist_ok=True)
     with open(FD.fixture_path(name), "w") as fh:

@@ -29,30 +29,46 @@ def _args(bench, argv):
 
 def test_default_workload_is_c2_full(bench):
     a = _args(bench, [])
-    fx = bench.matching_fixture(a, a.reads)
-    assert fx is not None and fx["config"] == "c2_full"
-    # strong scaling over 8 ranks is the same stream
-    a8 = _args(bench, ["--gpus", "8", "--strong"])
-    assert bench.matching_fixture(a8, 8 * ((a8.reads + 7) // 8))["config"] == "c2_full"
+    fx, exact = bench.matching_fixture(a, a.reads)
+    assert fx is not None and fx["config"] == "c2_full" and exact
+    # strong scaling over 8 ranks is the same stream (broadcast mode: rank order)
+    a8 = _args(bench, ["--gpus", "8", "--strong", "--group-mode", "broadcast"])
+    assert bench.matching_fixture(a8, 8 * ((a8.reads + 7) // 8)) == (bench.matching_fixture(a, a.reads)[0], True)
     # weak scaling at 8 ranks: 400M reads, no fixture
-    assert bench.matching_fixture(a8, 8 * a8.reads) is None
+    assert bench.matching_fixture(a8, 8 * a8.reads) == (None, False)
+
+
+def test_exchange_fixture_order(bench):
+    """Exchange mode's pass-interleaved stream: the fixture made in that
+    order (c2_full_x2b: 2 ranks at the default batch) is an exact match; with
+    none for the order (8 ranks at the default batch) the rank-order fixture
+    checks the order-free outputs only."""
+    a = _args(bench, ["--gpus", "2", "--strong"])
+    fx, exact = bench.matching_fixture(a, 50_000_000, [2, a.batch_kmers])
+    assert fx["config"] == "c2_full_x2b" and exact
+    fx, exact = bench.matching_fixture(a, 50_000_000, [8, a.batch_kmers])
+    assert fx["config"] == "c2_full" and not exact
+    part = bench.compare_fixture(fx, 1, fx["n_occupied"], fx["table_sha256"], stream_order=False)
+    assert part["n_occupied_match"] and part["tables_match"] and "counters_match" not in part
 
 
 @pytest.mark.parametrize("argv,name", [(["--config", "C3", "--reads", "4000000"], "c3_shape"),
                                        (["--config", "C4", "--reads", "4000000"], "c4_shape"),
                                        (["--config", "C5", "--reads", "4000000"], "c5_shape"),
+                                       (["--config", "C5", "--reads", "4000000", "--genome", "5e7"], "c5_genomic"),
+                                       (["--config", "C5M", "--reads", "1000000", "--genome", "1e7"], "c5m_genomic"),
                                        (["--genome", "2e6", "--reads", "10000000"], "genomic_c2"),
                                        (["--reads", "49999999"], None),
                                        (["--no-bigcount"], None)])
 def test_fixture_match(bench, argv, name):
     a = _args(bench, argv)
-    fx = bench.matching_fixture(a, a.reads)
+    fx, _ = bench.matching_fixture(a, a.reads)
     assert (fx["config"] if fx else None) == name
 
 
 def test_compare_fixture(bench):
     a = _args(bench, [])
-    fx = bench.matching_fixture(a, a.reads)
+    fx, _ = bench.matching_fixture(a, a.reads)
     ok = bench.compare_fixture(fx, fx["n_unique_kmers"], fx["n_occupied"], fx["table_sha256"])
     assert ok == {"fixture": "c2_full", "counters_match": True, "tables_match": True}
     bad = bench.compare_fixture(fx, fx["n_unique_kmers"] + 1, fx["n_occupied"], None)
