@@ -354,8 +354,6 @@ def main():
         args.reads = (args.reads + world - 1) // world   # per rank
     nreads = args.reads
     nkmers = nreads * (L - k + 1)
-    if args.query and world > 1:
-        raise SystemExit("--query runs on one GPU")
     sizes = khmer_amd.get_n_primes_near_x(nt, args.x)
 
     if world > 1:
@@ -398,8 +396,10 @@ def main():
     if args.query:
         # the tables were built untimed from the same reads; the fixture's
         # get_median_count digest (median, average, stddev of its first reads)
-        if fx is not None and fx.get("median_sha256") and rank == 0:
-            check_info.update(runner.query_check(fx))
+        if fx is not None and fx.get("median_sha256"):
+            q = runner.query_check(fx)   # collective when sharded
+            if rank == 0:
+                check_info.update(q)
         fx = None
     if fx is not None:
         sha = runner.table_sha256()   # collective when sharded

@@ -746,28 +746,6 @@ static uint64_t own_filter(Graph *g, const Src &src, uint64_t nkmers, bool windo
     }
 }
 
-// register-direct level 1 (k_scatter_l1r): KH_L1R=1 (two 1024-thread
-// workgroups per CU, <= 64 VGPRs), 2 (one per CU), 0 off
-static int l1r_mode() { static const int v = env_seg("KH_L1R", 0); return v; }
-static size_t lds_scatter_l1r(const Params &P) { return (size_t)P.F1 * (8 + 8 + 16 * 8 + 4 + 4 + 2) + 16 + 64; }
-template <class Src>
-static L1FFn<Src> l1r_kernel(int kpt, int mode) {
-    if (mode == 1) {
-        switch (kpt) {
-            case 1: return k_scatter_l1r<Src, 1, 8>;
-            case 2: return k_scatter_l1r<Src, 2, 8>;
-            case 4: return k_scatter_l1r<Src, 4, 8>;
-            default: return k_scatter_l1r<Src, 8, 8>;
-        }
-    }
-    switch (kpt) {
-        case 1: return k_scatter_l1r<Src, 1, 4>;
-        case 2: return k_scatter_l1r<Src, 2, 4>;
-        case 4: return k_scatter_l1r<Src, 4, 4>;
-        default: return k_scatter_l1r<Src, 8, 4>;
-    }
-}
-
 // k_scatter_l1f over every level-1 window (l1f_windows) of graph g's
 // geometry: records of k-mer j carry index jbase + j
 template <class Src>
@@ -776,22 +754,6 @@ static void launch_l1f(Graph *g, const Src &src, uint64_t nkmers, bool window, u
     const int rpt = l1f_rpt();
     for (const L1Win &wn : l1f_windows(g->prm, l1f_tables_per_launch())) {
         const Params Q = win_params(g->prm, wn);
-        const int l1r = l1r_mode();
-        if (l1r && !window && Q.F1 <= (uint32_t)L1R_MAX_F1) {
-            int kpt = 1;
-            while (kpt * 2 * wn.nt <= 8) kpt *= 2;
-            const uint64_t tk = (uint64_t)L1R_THREADS * kpt;
-            const uint64_t per_cu = std::min<uint64_t>(l1r == 1 ? 2 : 1, 163840 / lds_scatter_l1r(Q));
-            const uint32_t nwg = (uint32_t)std::max<uint64_t>(
-                1, std::min<uint64_t>((nkmers + tk - 1) / tk / 4 + 1, std::max<uint64_t>(1, per_cu) * device_cus(g)));
-            const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
-            KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, g->stream));
-            TIMED("scatter_l1", hipLaunchKernelGGL(l1r_kernel<Src>(kpt, l1r), dim3(nwg), dim3(L1R_THREADS),
-                                                   lds_scatter_l1r(Q), g->stream, Q, src, nkmers, kpw, wn.t0, wn.nt,
-                                                   w.bkt_base + wn.bb0, (unsigned long long *)w.bkt_cur + wn.bb0,
-                                                   w.rec1, w.ctr, l1f_blk_sh(), jbase, l1f_chunk_tiles(g)));
-            continue;
-        }
         const uint32_t nwg = l1f_workgroups_q(g, Q, nkmers);
         int kpt = 1;
         while (kpt * 2 * wn.nt <= rpt) kpt *= 2;
@@ -1789,12 +1751,6 @@ static void set_lds_limits() {
         KH_LDS_MAX(l1f_kernel<SrcHashes>(kpt, 8));
     }
     KH_LDS_MAX((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>));
-    for (int kpt : {1, 2, 4, 8})
-        for (int mode : {1, 2}) {
-            KH_LDS_MAX(l1r_kernel<SrcTwoBit>(kpt, mode));
-            KH_LDS_MAX(l1r_kernel<SrcBytes>(kpt, mode));
-            KH_LDS_MAX(l1r_kernel<SrcHashes>(kpt, mode));
-        }
     for (int kpt : {1, 2, 4, 8}) {
         KH_LDS_MAX(own_l1f_kernel<SrcTwoBit>(kpt, false));
         KH_LDS_MAX(own_l1f_kernel<SrcTwoBit>(kpt, true));

@@ -834,205 +834,6 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
 }
 
 // ---------------------------------------------------------------------------
-// Level 1, register-direct: k_scatter_l2f's scheme applied to the hashing
-// level.  No LDS staging, no run-start scan: every thread hashes KPT k-mers
-// (the next tile's input is fetched a tile ahead), ranks its RPT = 8 records
-// with LDS atomics on the tile histogram, and stores each record straight
-// from its register to the workgroup's block of the bucket, except the
-// records of a bucket's last partial 128-B segment, which wait in an LDS tail
-// until a later tile completes the segment (tails whose segment completes are
-// listed and flushed by 16 consecutive lanes each).  Blocks of 2^blk_sh
-// records are reserved per (bucket, tile) with one returning atomic, as in
-// k_scatter_l1f, and the same chunk queue distributes the tiles.  1024
-// threads; per-bucket LDS state ~154 B (F1 <= 512: two workgroups per CU).
-constexpr int L1R_THREADS = 1024;
-constexpr int L1R_MAX_F1 = 512;
-template <class Src, int KPT, int WPE>
-__global__ void __launch_bounds__(L1R_THREADS, WPE) k_scatter_l1r(Params P, Src src, uint64_t nkmers, uint64_t kpw,
-                                                                 int t0, int nt, const uint64_t *bkt_base,
-                                                                 unsigned long long *bkt_cur, uint64_t *rec,
-                                                                 uint64_t *ctr, int blk_sh, uint32_t jbase,
-                                                                 uint32_t cht) {
-    constexpr int THREADS = L1R_THREADS;
-    constexpr int RPT = 8;
-    constexpr int TILE_KMERS = THREADS * KPT;
-    constexpr uint32_t SEG = 16;
-    constexpr uint64_t DEAD = ~0ull;
-    const uint32_t BLK = 1u << blk_sh;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t F1 = P.F1;
-    uint64_t *bcur = (uint64_t *)smem;              // [F1] base of the partially filled block (DEAD: overflowed)
-    uint64_t *nbase = bcur + F1;                    // [F1] base of the blocks reserved for this tile
-    uint64_t *tail = nbase + F1;                    // [F1*SEG] pending partial segments
-    uint32_t *cnt = (uint32_t *)(tail + F1 * SEG);  // [F1] records appended by this workgroup
-    uint32_t *hist = cnt + F1;                      // [F1] this tile's records
-    uint32_t *s_nfl = hist + F1;                    // [0] entries of flist, [1] the chunk taken from the queue
-    uint16_t *flist = (uint16_t *)(s_nfl + 4);      // [F1] buckets whose pending tail completes this tile
-    const int shift = P.s0 + P.s2;
-    const uint64_t omask = (1ull << shift) - 1;
-    for (uint32_t d = threadIdx.x; d < F1; d += THREADS) {
-        bcur[d] = 0;
-        cnt[d] = 0;
-        hist[d] = 0;
-    }
-    if (threadIdx.x == 0) s_nfl[0] = 0;
-    // chunks of CK k-mers: a fixed share per workgroup (cht == 0) or chunks of
-    // cht tiles from the queue head ctr[CTR_L1Q], the next one known a chunk
-    // ahead (k_scatter_l1f)
-    const uint64_t CK = cht ? (uint64_t)cht * TILE_KMERS : kpw;
-    const uint32_t nchunks = (uint32_t)((nkmers + CK - 1) / CK);
-    uint32_t cb = cht ? blockIdx.x + gridDim.x : nchunks;
-    uint64_t j0 = min(nkmers, (uint64_t)blockIdx.x * CK);
-    uint64_t ce = min(nkmers, j0 + CK);
-    bool chunk_top = true;
-    typename Src::Pend pend[KPT];
-#pragma unroll
-    for (int a = 0; a < KPT; a++) {
-        const uint64_t j = j0 + (uint64_t)a * THREADS + threadIdx.x;
-        if (j < min(ce, j0 + TILE_KMERS)) pend[a] = kmer_fetch(src, j);
-    }
-    auto phys = [&](uint32_t d, uint32_t L) -> uint64_t {
-        const uint32_t split = (cnt[d] + BLK - 1) & ~(BLK - 1);
-        if (L < split) return bcur[d] == DEAD ? DEAD : bcur[d] + (L & (BLK - 1));
-        return nbase[d] == DEAD ? DEAD : nbase[d] + (L - split);
-    };
-    for (;j0 < ce;) {
-        const uint64_t j1 = min(ce, j0 + TILE_KMERS);
-        uint64_t n0 = j1, n1 = j1;
-        if (j1 < ce) {
-            n1 = min(ce, j1 + TILE_KMERS);
-        } else if (cb < nchunks) {
-            n0 = (uint64_t)cb * CK;
-            n1 = min(nkmers, n0 + min(CK, (uint64_t)TILE_KMERS));
-        }
-        const bool last = n1 == n0;   // the workgroup's final tile: every tail is flushed
-        unsigned long long qn = 0;
-        if (cht && chunk_top && threadIdx.x == 0) qn = atomicAdd((unsigned long long *)&ctr[CTR_L1Q], 1ull);
-        block_sync();
-        // records: v = (j << 32) | offset in the bucket, bk = bucket << 16 | tile rank
-        uint64_t v[RPT];
-        uint32_t bk[RPT];
-#pragma unroll
-        for (int q = 0; q < RPT; q++) bk[q] = ~0u;
-        uint64_t hh[KPT];
-#pragma unroll
-        for (int a = 0; a < KPT; a++) {
-            const uint64_t j = j0 + (uint64_t)a * THREADS + threadIdx.x;
-            hh[a] = j < j1 ? src.finish(pend[a]) : 0;
-        }
-#pragma unroll
-        for (int a = 0; a < KPT; a++) {
-            const uint64_t j = j0 + (uint64_t)a * THREADS + threadIdx.x;
-            const bool ok = j < j1;
-#pragma unroll
-            for (int q = 0; q < RPT; q++) {
-                const int i = q - a * nt;
-                if (ok && i >= 0 && i < nt) {
-                    uint64_t G;
-                    if (local_bin(P, t0 + i, hh[a], &G)) {
-                        const uint32_t d = (uint32_t)(G >> shift);
-                        v[q] = ((uint64_t)(jbase + (uint32_t)j) << 32) | (G & omask);
-                        bk[q] = (d << 16) | atomicAdd(&hist[d], 1u);
-                    }
-                }
-            }
-        }
-        // the next tile's input (loads in flight behind this tile's work)
-#pragma unroll
-        for (int a = 0; a < KPT; a++) {
-            const uint64_t j = n0 + (uint64_t)a * THREADS + threadIdx.x;
-            if (j < n1) pend[a] = kmer_fetch(src, j);
-        }
-        block_sync();
-        // blocks for this tile (thread d owns bucket d) and the buckets whose
-        // pending tail segment completes in this tile (every one on the last)
-        {
-            const uint32_t d = threadIdx.x;
-            bool fl = false;
-            if (d < F1) {
-                const uint32_t h = hist[d], c0 = cnt[d];
-                const bool dead = bcur[d] == DEAD;
-                if (h) {
-                    const uint32_t need = ((c0 + h + BLK - 1) >> blk_sh) - ((c0 + BLK - 1) >> blk_sh);
-                    uint64_t nb = 0;
-                    if (dead) {
-                        nb = DEAD;
-                    } else if (need) {
-                        nb = atomicAdd(&bkt_cur[d], (unsigned long long)need * BLK);
-                        if (nb + (uint64_t)need * BLK > bkt_base[d + 1]) {
-                            atomicOr((unsigned long long *)&ctr[CTR_ERR], 8ull);
-                            nb = DEAD;
-                        }
-                    }
-                    nbase[d] = nb;
-                }
-                const uint32_t a = c0 & ~(SEG - 1), e = c0 + h;
-                fl = !dead && c0 != a && (last ? e : (e & ~(SEG - 1))) > a;
-            }
-            const uint64_t m = __ballot(fl);
-            if (m) {
-                uint32_t base = 0;
-                if ((threadIdx.x & 63) == 0) base = atomicAdd(&s_nfl[0], (uint32_t)__popcll(m));
-                base = __shfl(base, 0, 64);
-                if (fl) flist[base + (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63)) - 1))] = (uint16_t)d;
-            }
-        }
-        if (cht && chunk_top && threadIdx.x == 0) s_nfl[1] = (uint32_t)min<unsigned long long>(qn + 2ull * gridDim.x, nchunks);
-        block_sync();
-        {
-            const uint32_t nfl = s_nfl[0];
-            for (uint32_t y = threadIdx.x; y < nfl * SEG; y += THREADS) {
-                const uint32_t d = flist[y / SEG], sl = y % SEG;
-                const uint32_t c0 = cnt[d], a = c0 & ~(SEG - 1);
-                if (a + sl < c0) rec[bcur[d] + ((a + sl) & (BLK - 1))] = tail[d * SEG + sl];
-            }
-        }
-        block_sync();   // the flushed tail slots are refilled below
-#pragma unroll
-        for (int q = 0; q < RPT; q++) {
-            if (bk[q] == ~0u) continue;
-            const uint32_t d = bk[q] >> 16;
-            const uint32_t L = cnt[d] + (bk[q] & 0xFFFFu);
-            const uint32_t e = cnt[d] + hist[d];
-            if (L < (last ? e : (e & ~(SEG - 1)))) {
-                const uint64_t pos = phys(d, L);
-                if (pos != DEAD) rec[pos] = v[q];
-            } else {
-                tail[d * SEG + (L & (SEG - 1))] = v[q];
-            }
-        }
-        block_sync();
-        if (threadIdx.x == 0) s_nfl[0] = 0;
-        for (uint32_t d = threadIdx.x; d < F1; d += THREADS) {
-            const uint32_t h = hist[d];
-            if (!h) continue;
-            const uint32_t c0 = cnt[d];
-            const uint32_t need = ((c0 + h + BLK - 1) >> blk_sh) - ((c0 + BLK - 1) >> blk_sh);
-            if (nbase[d] == DEAD) bcur[d] = DEAD;
-            else if (need) bcur[d] = nbase[d] + (uint64_t)(need - 1) * BLK;
-            cnt[d] = c0 + h;
-            hist[d] = 0;
-        }
-        chunk_top = j1 >= ce;
-        if (chunk_top) {
-            j0 = n0;
-            ce = cb < nchunks ? min(nkmers, (uint64_t)cb * CK + CK) : n0;
-            cb = cht ? uniform_u32(s_nfl[1]) : nchunks;
-        } else {
-            j0 = j1;
-        }
-    }
-    // the rest of every partially filled block: sentinels
-    block_sync();
-    for (uint32_t y = threadIdx.x; y < F1 * BLK; y += THREADS) {
-        const uint32_t d = y >> blk_sh, sl = y & (BLK - 1);
-        const uint32_t c = cnt[d] & (BLK - 1);
-        if (c == 0 || sl < c || bcur[d] == DEAD) continue;
-        rec[bcur[d] + sl] = ~0ull;
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Level 1 of a shard ("owned filter").  A shard of a G-rank group owns ~1/G
 // of every table's bins but hashes every k-mer of the stream, so with
 // k_hist_l1 + k_scatter_l1 it would hash each k-mer twice and run the whole

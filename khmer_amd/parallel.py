@@ -347,10 +347,11 @@ class ShardedCountgraphBench(object):
 
     def config_name(self):
         a = self.args
-        return a.graph + " k=%d %dx%.0e sharded over %dxMI355X%s, %d x %d bp synthetic %sreads per GPU%s" % (
+        return a.graph + " k=%d %dx%.0e sharded over %dxMI355X%s, %s%d x %d bp synthetic %sreads per GPU%s" % (
             a.k, a.tables, a.x, self.world,
             " (exchange: each rank hashes its own reads, buckets sent to owners)" if getattr(a, "exchange", False)
-            else "", a.reads, a.read_len, "genomic " if a.genome else "",
+            else "", "get_median_count over " if a.query else "", a.reads, a.read_len,
+            "genomic " if a.genome else "",
             " (strong scaling: %d reads in all)" % (a.reads * self.world) if a.strong else "")
 
     def setup(self):
@@ -381,16 +382,57 @@ class ShardedCountgraphBench(object):
         check(lib.kh_device_malloc(self.device, nwords * 8, ctypes.byref(self.words)))
         check(lib.kh_device_malloc(self.device, (a.reads + 1) * 8, ctypes.byref(self.koff)))
         # every rank's own reads: the rank-th block of the synthetic stream
+        ks = min(a.k, 32)   # the packed stream itself does not depend on k
         if a.genome:
             check(lib.kh_synth_genomic_device(self.device, synth.SEED, a.genome, self.rank * a.reads, a.reads,
-                                              a.read_len, a.k, self.words, self.koff))
+                                              a.read_len, ks, self.words, self.koff))
         else:
-            check(lib.kh_synth_packed_device(self.device, synth.SEED, self.rank * a.reads, a.reads, a.read_len, a.k,
+            check(lib.kh_synth_packed_device(self.device, synth.SEED, self.rank * a.reads, a.reads, a.read_len, ks,
                                              self.words, self.koff))
+        self.reads = self.words
+        self.outs = None
+        if self.g.murmur:   # the Counttable family hashes ASCII: the same bases unpacked
+            self.ascii = ctypes.c_void_p()
+            check(lib.kh_device_malloc(self.device, a.reads * a.read_len + 64, ctypes.byref(self.ascii)))
+            check(lib.kh_unpack_ascii_device(self.device, self.words, a.reads * a.read_len, self.ascii))
+            self.reads = self.ascii
+        if a.query:
+            self.outs = ctypes.c_void_p()
+            check(lib.kh_device_malloc(self.device, a.reads * 10 + 64, ctypes.byref(self.outs)))
+            self._consume()   # the tables being queried (untimed)
+
+    def _consume(self):
+        a = self.args
+        if self.g.murmur:
+            self.g.consume_bytes_fixed_device([self.reads], a.reads, a.read_len)
+        else:
+            self.g.consume_packed_fixed_device([self.words], a.reads, a.read_len)
 
     def step(self):
+        a = self.args
+        if a.query:
+            o = self.outs.value
+            self.g.median_fixed_device([self.reads], a.reads, a.read_len, [o], [o + 2 * a.reads], [o + 6 * a.reads])
+            return
         self.g.clear()
-        self.g.consume_packed_fixed_device([self.words], self.args.reads, self.args.read_len)
+        self._consume()
+
+    def query_check(self, fx):
+        """The fixture's get_median_count digest over its first median_reads
+        reads, from every rank's outputs in rank order (collective)."""
+        import numpy as np
+        from tests import full_digest as FD
+        n = self.args.reads
+        raw = (ctypes.c_uint8 * (n * 10))()
+        check(lib.kh_device_synchronize(self.device))
+        check(lib.kh_device_copy(self.device, raw, self.outs, n * 10))
+        parts = self.rdv.allgather(bytes(raw))
+        med = np.concatenate([np.frombuffer(p[:2 * n], np.uint16) for p in parts])
+        avg = np.concatenate([np.frombuffer(p[2 * n:6 * n], np.float32) for p in parts])
+        sd = np.concatenate([np.frombuffer(p[6 * n:], np.float32) for p in parts])
+        m = fx["median_reads"]
+        return {"fixture": fx["config"], "median_reads": m,
+                "median_match": FD.median_digest(med[:m], avg[:m], sd[:m]) == fx["median_sha256"]}
 
     def sync(self):
         check(lib.kh_device_synchronize(self.device))
@@ -443,6 +485,10 @@ class ShardedCountgraphBench(object):
     def close(self):
         lib.kh_device_free(self.device, self.words)
         lib.kh_device_free(self.device, self.koff)
+        if self.g.murmur:
+            lib.kh_device_free(self.device, self.ascii)
+        if self.outs is not None:
+            lib.kh_device_free(self.device, self.outs)
         self.g.close()
         self.rdv.close()
 

@@ -21,7 +21,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
-KINDS = {"Countgraph": 1, "Nodegraph": 2, "SmallCountgraph": 7}
+KINDS = {"Countgraph": 1, "Nodegraph": 2, "SmallCountgraph": 7, "Counttable": 1, "SmallCounttable": 7}
 
 
 def _rank_main():
@@ -44,16 +44,37 @@ def _rank_main():
     words, koff = ctypes.c_void_p(), ctypes.c_void_p()
     check(lib.kh_device_malloc(0, (n * L // 32 + 2) * 8, ctypes.byref(words)))
     check(lib.kh_device_malloc(0, (n + 1) * 8, ctypes.byref(koff)))
+    ks = min(k, 32)
     if cfg["genome"]:
-        check(lib.kh_synth_genomic_device(0, synth.SEED, cfg["genome"], rank * n, n, L, k, words, koff))
+        check(lib.kh_synth_genomic_device(0, synth.SEED, cfg["genome"], rank * n, n, L, ks, words, koff))
     else:
-        check(lib.kh_synth_packed_device(0, synth.SEED, rank * n, n, L, k, words, koff))
-    g.consume_packed_fixed_device([words], n, L)
+        check(lib.kh_synth_packed_device(0, synth.SEED, rank * n, n, L, ks, words, koff))
+    reads = words
+    if g.murmur:   # the Counttable family: ASCII reads
+        reads = ctypes.c_void_p()
+        check(lib.kh_device_malloc(0, n * L + 64, ctypes.byref(reads)))
+        check(lib.kh_unpack_ascii_device(0, words, n * L, reads))
+        g.consume_bytes_fixed_device([reads], n, L)
+    else:
+        g.consume_packed_fixed_device([words], n, L)
     u, occ = g.counters()
     tabs = g.gather_tables(rdv)
     bc = g.shards[0].bigcounts()
     out = {"rank": rank, "n_unique": u, "n_occupied": occ, "bigcounts": [[int(a), int(b)] for a, b in bc],
            "comm": g.comm_info()}
+    if cfg.get("query"):   # the sharded get_median_count of this rank's own reads
+        import numpy as np
+        q = ctypes.c_void_p()
+        check(lib.kh_device_malloc(0, n * 10 + 64, ctypes.byref(q)))
+        g.median_fixed_device([reads], n, L, [q.value], [q.value + 2 * n], [q.value + 6 * n])
+        raw = (ctypes.c_uint8 * (n * 10))()
+        check(lib.kh_device_copy(0, raw, q, n * 10))
+        lib.kh_device_free(0, q)
+        b = bytes(raw)
+        out["median"] = np.frombuffer(b[:2 * n], np.uint16).tolist()
+        out["avg_sd_hex"] = b[2 * n:].hex()
+    if g.murmur:
+        lib.kh_device_free(0, reads)
     if rank == 0:
         import hashlib
         out["tables"] = [hashlib.sha256(t).hexdigest() for t in tabs]
@@ -72,23 +93,33 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("cls,world,bigcount,exchange", [("Countgraph", 2, True, False), ("Countgraph", 3, True, False),
-                                                         ("Nodegraph", 2, False, False),
-                                                         ("SmallCountgraph", 3, False, False),
-                                                         ("Countgraph", 2, True, True), ("Countgraph", 3, True, True),
-                                                         ("Nodegraph", 2, False, True)])
-def test_hosted_group_multiprocess(cls, world, bigcount, exchange):
+@pytest.mark.parametrize("cls,world,bigcount,exchange,query",
+                         [("Countgraph", 2, True, False, False), ("Countgraph", 3, True, False, False),
+                          ("Nodegraph", 2, False, False, False),
+                          ("SmallCountgraph", 3, False, False, False),
+                          ("Countgraph", 2, True, True, False), ("Countgraph", 3, True, True, False),
+                          ("Nodegraph", 2, False, True, False),
+                          # the Counttable family and the sharded get_median_count (round 4)
+                          ("SmallCounttable", 2, False, False, True), ("SmallCounttable", 3, False, True, True),
+                          ("Counttable", 2, True, True, True), ("Countgraph", 3, True, False, True)])
+def test_hosted_group_multiprocess(cls, world, bigcount, exchange, query):
     """exchange=True: Option A through the host transport's alltoallv (the
-    oracle consumes the pass-interleaved stream, parallel.exchange_passes)."""
+    oracle consumes the pass-interleaved stream, parallel.exchange_passes).
+    query=True: every rank's get_median_count of its own reads through the
+    host transport's MIN reduce (broadcast) / reduce-scatter (exchange),
+    against the oracle's per-read (median, average, stddev) bit patterns."""
     import hashlib
+    import numpy as np
     from oracle import oracle as O
     from khmer_amd import parallel, synth
+    murmur = cls in parallel.MURMUR_CLASSES
+    k = 51 if cls == "SmallCounttable" else 21
     sizes = O.get_n_primes_near_x(4, 100003)
     # bigcount cases read a 6 kbp genome (every k-mer ~400x, past 255 in all
-    # tables); the others the iid stream
-    genome = 6000 if bigcount else 0
-    cfg = {"cls": cls, "k": 21, "sizes": sizes, "batch": 1 << 20, "bigcount": bigcount, "nreads": 20000, "L": 150,
-           "genome": genome, "exchange": exchange}
+    # tables); the query cases a 40 kbp genome; the others the iid stream
+    genome = 6000 if bigcount else 40000 if query else 0
+    cfg = {"cls": cls, "k": k, "sizes": sizes, "batch": 1 << 20, "bigcount": bigcount, "nreads": 20000, "L": 150,
+           "genome": genome, "exchange": exchange, "query": query}
     port = _free_port()
     procs = []
     for r in range(world):
@@ -106,10 +137,10 @@ def test_hosted_group_multiprocess(cls, world, bigcount, exchange):
             raise
         assert p.returncode == 0, so[-3000:]
         outs.append(json.loads([ln for ln in so.splitlines() if ln.startswith("RESULT ")][-1][7:]))
-    o = O.Table(KINDS[cls], 21, sizes)
+    o = O.Table(KINDS[cls], k, sizes, hash=O.MURMUR if murmur else O.TWOBIT)
     o.set_use_bigcount(bigcount)
     n = cfg["nreads"]
-    order = ([(s * n + r0, nr) for r0, nr in parallel.exchange_passes(n, cfg["L"], 21, world, cfg["batch"])
+    order = ([(s * n + r0, nr) for r0, nr in parallel.exchange_passes(n, cfg["L"], k, world, cfg["batch"])
               for s in range(world)] if exchange else [(s * n, n) for s in range(world)])
     for start, cnt in order:
         if genome:
@@ -126,3 +157,18 @@ def test_hosted_group_multiprocess(cls, world, bigcount, exchange):
         assert x["comm"] == [0, -1]   # no RCCL in a host-transport group
     if bigcount:
         assert ref_bc, "the case should exercise the bigcount merge"
+    if query:
+        L = cfg["L"]
+        got_med = np.concatenate([np.array(x["median"], np.uint16) for x in sorted(outs, key=lambda x: x["rank"])])
+        got_f = b"".join(bytes.fromhex(x["avg_sd_hex"]) for x in sorted(outs, key=lambda x: x["rank"]))
+        want_med, want_f = [], b""
+        for s in range(world):
+            seqs = synth.genomic_batch(s * n, n, L, genome)[0]
+            m, a, d = np.zeros(n, np.uint16), np.zeros(n, np.float32), np.zeros(n, np.float32)
+            for r in range(n):
+                m[r], a[r], d[r] = o.median(seqs[r * L:(r + 1) * L])
+            want_med.append(m)
+            want_f += a.tobytes() + d.tobytes()
+        assert np.array_equal(got_med, np.concatenate(want_med))
+        assert got_f == want_f
+        assert int(got_med.max()) > 2

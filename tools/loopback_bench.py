@@ -5,8 +5,8 @@ device, device copies instead of RCCL broadcasts) over G x R synthetic reads
 (weak scaling: R reads per source rank), and prints the wall time per step
 divided by G -- the compute time one rank of a real G-GPU group spends, minus
 the broadcast -- with the per-kernel breakdown summed over shards / G.
-Usage: python tools/loopback_bench.py [world] [reads_per_rank] [steps] [batch_kmers] [exchange]
-(exchange = 1: Option A, kh_group_create_mode KH_GROUP_EXCHANGE)
+Usage: python tools/loopback_bench.py [world] [reads_per_rank] [steps] [batch_kmers] [exchange] [x]
+(exchange = 1: Option A, kh_group_create_mode KH_GROUP_EXCHANGE; x: table size, 1e9 = C2, 8e9 = C4)
 """
 import ctypes
 import json
@@ -24,8 +24,9 @@ reads = int(sys.argv[2]) if len(sys.argv) > 2 else 50_000_000
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 batch = int(sys.argv[4]) if len(sys.argv) > 4 else 3200 << 20
 exchange = len(sys.argv) > 5 and sys.argv[5] == "1"
+x = float(sys.argv[6]) if len(sys.argv) > 6 else 1e9
 L, k = 150, 21
-sizes = khmer_amd.get_n_primes_near_x(4, 1e9)
+sizes = khmer_amd.get_n_primes_near_x(4, x)
 g = parallel.ShardedGraph("Countgraph", k, sizes, world, loopback=True, exchange=exchange)
 g.set_use_bigcount(True)
 g.set_batch_kmers(batch)
