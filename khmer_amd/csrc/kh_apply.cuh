@@ -1156,6 +1156,19 @@ __global__ void k_window_starts(const uint64_t *O3, const uint32_t *M3, uint32_t
     }
 }
 
+// the same from the coarse-window path's [coarse][fine][chunk] matrix
+// (k_hist_wf / k_scatter_wf): fine window w = c * fpc + f starts at
+// O[cmbase[c] + f * cnk[c]]; a coarse window without chunks, and every window
+// past the last winner, starts at the running total (O has one entry past
+// the matrix, and cmbase[c] = that entry for c >= the pass's coarse windows)
+__global__ void k_window_starts_cw(const uint64_t *O, const uint64_t *cmbase, const uint32_t *cnk, uint32_t fpc,
+                                   uint32_t FJ, uint64_t *ws) {
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w <= FJ; w += gridDim.x * blockDim.x) {
+        const uint32_t c = w / fpc, f = w % fpc;
+        ws[w] = c < MAX_CW ? O[cmbase[c] + (uint64_t)f * cnk[c]] : O[cmbase[MAX_CW]];
+    }
+}
+
 // k_mark over windows [wlo, wlo + gridDim.x) whose winners arrived from G
 // shards: source s's part of window w is recv[roff[s] + ws_s[w] - ws_s[wlo] ...)
 __global__ void __launch_bounds__(PT_THREADS) k_mark_multi(const uint32_t *recv, const uint64_t *ws_all,

@@ -804,12 +804,14 @@ struct PassState {
 };
 
 // The coarse-window winner path (k_apply_count with A.coarse, k_hist_wf,
-// k_scatter_wf, k_mark_wf) for unsharded Byte/Nibble passes; KH_WINNERS=1
-// keeps the per-region winner lists (development; sharded groups always do,
-// their windows are routed across ranks)
+// k_scatter_wf, k_mark_wf); KH_WINNERS=1 keeps the per-region winner lists
+// (development).  Sharded groups route the fine windows of either layout
+// (group_route_winners: k_window_starts / k_window_starts_cw); pass_apply
+// decides per pass whether the coarse layout fits a shard's buffer.
 static bool coarse_winners(const Graph *g) {
     static const bool off = env_seg("KH_WINNERS", 0) == 1;
-    return !off && g->world == 1 && !g->grouped;
+    (void)g;
+    return !off;
 }
 
 // coarse-window runs -> fine windows: the windows' counts (one small copy),
@@ -893,9 +895,15 @@ static void pass_apply(Graph *g, PassState &ps, bool l2f) {
     // coarse windows of 2^cjs k-mers (<= 64), each a fine window multiple;
     // window c may hold (its k-mers) x (tables) winners, the capacity of its
     // range of the winner array (the dead level-1 records)
-    ps.coarse = coarse_winners(g);
-    A.coarse = ps.coarse ? 1 : 0;
     A.cjs = std::max(q.js, ceil_log2(nkmers) - 6);
+    // A coarse window's range of the winner array holds (its k-mers) x
+    // (tables) winners, a hard bound that sums to the pass's k-mers x tables:
+    // an unsharded pass's record count, which the dead level-1 buffer holds.
+    // A shard (or an exchange-mode owner) holds ~1/G of the records, so it
+    // takes the coarse path only when that bound still fits its buffer, and
+    // the per-region lists otherwise (their capacity is the region's records).
+    ps.coarse = coarse_winners(g) && (!g->grouped || nkmers * (uint64_t)P.n <= w.cap_recs);
+    A.coarse = ps.coarse ? 1 : 0;
     A.wco = win;
     A.cw_cur = nullptr;
     A.dyn = apply_dynamic(g) ? 1 : 0;
@@ -1012,8 +1020,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     bool l1f = false;
     uint64_t nrec = 0;   // records this pass writes (exact level 1 only)
     for (;;) {
-        l1f = fast && l1f_ok(g) &&
-              (std::is_same<Src, SrcHashes>::value || l1f_windows(P, l1f_tables_per_launch()).size() == 1);
+        l1f = fast && l1f_ok(g) && (std::is_same<Src, SrcHashes>::value || P.F1 <= 1024);
         const bool ownf = fast && !window && use_own_filter(g) && own_l1f_on();
         const uint64_t cap1 = (l1f || ownf) ? bkt_plan(g, nkmers) : 0;
         // level 1
@@ -2133,8 +2140,12 @@ static void group_route_winners(ShardGroup *G, std::vector<PassState> &ps) {
         ensure((void **)&lc.ws, &lc.cap_ws, FJ + 1, 8);
         ensure((void **)&lc.ws_all, &lc.cap_ws_all, (uint64_t)W * (FJ + 1), 8);
         ensure((void **)&lc.roff, &lc.cap_roff, W, 8);
-        TIMED("route", hipLaunchKernelGGL(k_window_starts, dim3((FJ + 256) / 256), dim3(256), 0, g->stream,
-                                          g->ws.moff, g->ws.mcnt, ps[l].q.nchw, FJ, lc.ws));
+        if (ps[l].coarse)
+            TIMED("route", hipLaunchKernelGGL(k_window_starts_cw, dim3((FJ + 256) / 256), dim3(256), 0, g->stream,
+                                              g->ws.moff, g->ws.cmbase, g->ws.cnk, ps[l].fpc, FJ, lc.ws));
+        else
+            TIMED("route", hipLaunchKernelGGL(k_window_starts, dim3((FJ + 256) / 256), dim3(256), 0, g->stream,
+                                              g->ws.moff, g->ws.mcnt, ps[l].q.nchw, FJ, lc.ws));
     }
     G->h_ws.assign((size_t)W * (FJ + 1), 0);
     if (per_rank(G)) {
@@ -2382,7 +2393,7 @@ static void a2a_level1(Graph *V, const Src &src, uint64_t nkmers, uint32_t jbase
     const PassGeo q = pass_geo(P, nkmers);
     ws_prepare(V, q);
     const uint64_t F1 = P.F1;
-    w.l1_exact = !std::is_same<Src, SrcHashes>::value && l1f_windows(P, l1f_tables_per_launch()).size() > 1;
+    w.l1_exact = !std::is_same<Src, SrcHashes>::value && P.F1 > 1024;
     if (w.l1_exact) {
         // more than 1024 buckets (C4 / C5 tables): the exact two-pass level 1
         // (as pass_stage_a) -- bucket b's records are [off1[b], off1[b + 1])

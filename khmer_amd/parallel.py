@@ -323,6 +323,27 @@ class ShardedGraph(object):
         """[[slice bytes per table] per local shard]."""
         return [[s.table_bytes(i) for i in range(len(self.sizes))] for s in self.shards]
 
+    def table_sha256(self):
+        """SHA-256 of every reference-layout table of a loopback (or 1-rank)
+        group, hashed slice by slice in rank order: no table is assembled in
+        host memory (C4's 8 GB tables)."""
+        import hashlib
+        if not (self.loopback or self.world == 1):
+            raise ValueError("table_sha256: loopback groups only (ShardedCountgraphBench.table_sha256 otherwise)")
+        out = []
+        for i, p in enumerate(self.sizes):
+            h = hashlib.sha256()
+            for r, (lo, size) in enumerate(self.rank_slices(i)):
+                sh = self.shards[r]
+                n = ctypes.c_uint64()
+                check(lib.kh_graph_table_nbytes(sh._g, i, ctypes.byref(n)))
+                buf = (ctypes.c_uint8 * max(n.value, 1))()
+                check(lib.kh_graph_copy_table(sh._g, i, buf))
+                h.update(memoryview(buf).cast("B")[:_slice_nbytes(self.kind, lo, size, p)])
+                del buf
+            out.append(h.hexdigest())
+        return out
+
     def gather_tables(self, rdv=None):
         """Reference-layout table bytes of the whole group.  Loopback: from the
         local shards; one process per rank: every rank's slices through the

@@ -166,8 +166,15 @@ def consume_full_fixture(fx, world, exchange, batch, fxname=None):
     rank order (the fixture's own stream order); exchange mode's stream is
     pass-interleaved, so its fixture is the one generated in that order
     (tests/full_digest.EXCHANGE)."""
-    import hashlib
+    import sys
+    import time
     from tests import full_digest as FD
+    t0 = time.time()
+
+    def note(what):   # progress on stderr (pytest -s): long GPU tests keep writing
+        sys.stderr.write("  [%s G=%d %s] %s at %.1f s\n" % (fx["config"], world, "exchange" if exchange else
+                                                          "broadcast", what, time.time() - t0))
+        sys.stderr.flush()
     c = fx["params"]
     if exchange:
         assert c["exchange"] == [world, batch], "the fixture was made for another pass interleave"
@@ -190,13 +197,14 @@ def consume_full_fixture(fx, world, exchange, batch, fxname=None):
             else:
                 check(lib.kh_synth_packed_device(0, fx["seed"], s * per, per, c["L"], c["k"], d.words, d.koff))
             srcs.append(d)
+        note("reads ready")
         g.consume_packed_fixed_device([d.words for d in srcs], per, c["L"])
         srcs = []
+        note("consumed")
         u, occ = g.counters()
         assert (u, occ) == (fx["n_unique_kmers"], fx["n_occupied"])
-        tabs = g.gather_tables()
-        assert [hashlib.sha256(t).hexdigest() for t in tabs] == fx["table_sha256"]
-        del tabs
+        assert g.table_sha256() == fx["table_sha256"]
+        note("tables hashed")
         if c["bigcount"]:
             for sh in g.shards:   # replicated on every rank
                 assert FD.bigcount_digest(dict(sh.bigcounts())) == (fx["n_bigcounts"], fx["bigcount_sha256"])
@@ -418,7 +426,6 @@ def test_loopback_c5m(name, world, mode):
     fixtures (exchange mode: the pass-interleaved c5m_*_x2 / _x8), then the sharded
     get_median_count of all its reads against the fixture's (median,
     average, stddev) digest.  c5m_genomic's medians spread over 1..15."""
-    import hashlib
     import numpy as np
     from tests import full_digest as FD
     fx = FD.load(name)
@@ -437,9 +444,7 @@ def test_loopback_c5m(name, world, mode):
         g.consume_bytes_fixed_device([s.ascii for s in srcs], per, c["L"])
         u, occ = g.counters()
         assert (u, occ) == (fxo["n_unique_kmers"], fx["n_occupied"])
-        tabs = g.gather_tables()
-        assert [hashlib.sha256(t).hexdigest() for t in tabs] == fx["table_sha256"]
-        del tabs
+        assert g.table_sha256() == fx["table_sha256"]
         nq = fx["median_reads"]
         assert nq == c["reads"]
         med, avg, sd = group_query(g, srcs, per, c["L"], True)

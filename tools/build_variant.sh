@@ -7,9 +7,9 @@ set -euo pipefail
 name=${1:?name}; flags=${2:-}
 root="$(cd "$(dirname "$0")/.." && pwd)"
 tmp=/tmp/kh_variant_$name
-rm -rf "$tmp"; mkdir -p "$tmp/khmer_amd" "$root/ab"
+rm -rf "$tmp"; mkdir -p "$tmp/khmer_amd" "$root/${KH_VARIANT_DIR:-ab}"
 cp -r "$root/include" "$tmp/include"
 cp -r "$root/khmer_amd/csrc" "$tmp/khmer_amd/csrc"
 rm -rf "$tmp/khmer_amd/csrc/build"
-make -s -C "$tmp/khmer_amd/csrc" -j4 OUT="$root/ab/lib$name.so" EXTRA_HIPFLAGS="$flags"
-echo "built ab/lib$name.so"
+make -s -C "$tmp/khmer_amd/csrc" -j4 OUT="$root/${KH_VARIANT_DIR:-ab}/lib$name.so" EXTRA_HIPFLAGS="$flags"
+echo "built ${KH_VARIANT_DIR:-ab}/lib$name.so"

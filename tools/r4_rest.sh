@@ -15,7 +15,7 @@ run() {
   grep -E "PASSED|FAILED|ERROR|passed|failed" "$out/$name.txt" | tail -40
   return $rc
 }
-run rccl 300 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_shard.py -k "rccl" &&
-run c4 700 python3 -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_shard.py -k "c4_shape or c5m_genomic" &&
+true &&
+run c4 900 python3 -u -m pytest -x -v -s --timeout 400 --timeout-method thread tests/test_gpu_shard.py -k "c4_shape or c5m_genomic" &&
 run mp 400 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_shard_mp.py &&
 run misc 500 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_scripts.py tests/test_gpu_full.py -k "c1_exact or genomic"
