@@ -245,34 +245,77 @@ int kh_graph_set_batch_kmers(kh_graph *h, uint64_t max_kmers) {
 }  // extern "C"
 
 // ---------------- consume helpers -------------------------------------------------
+std::vector<uint64_t> TagSet::sorted() const {
+    std::vector<uint64_t> v;
+    v.reserve(size());
+    for (uint64_t x : slot_)
+        if (x != EMPTY) v.push_back(x);
+    if (has_empty_) v.push_back(EMPTY);
+    std::sort(v.begin(), v.end());
+    return v;
+}
+
 // Hashgraph::consume_sequence_and_tag state machine (src/oxli/hashgraph.cc:200-271)
-// over one batch: is-new flags and hashes come from the device pass.
-static uint64_t tag_batch(Graph *g, const HostBatch &b, const uint8_t *isnew, const uint64_t *hashes) {
+// over one batch: the is-new flags come from the device pass as a bitmap.  A
+// k-mer's hash is needed only where the machine looks at it -- a k-mer that
+// is not new (tag membership), a tag position, a read's last k-mer -- and is
+// computed here from the batch's own reads (kh_device.h: the device's
+// arithmetic), so no per-k-mer hash leaves the device.  Runs of new k-mers
+// advance `since` arithmetically: a tag every density - 1 new k-mers.
+static uint64_t tag_batch(Graph *g, const HostBatch &b, const uint32_t *nb) {
     const uint32_t density = 40;  // DEFAULT_TAG_DENSITY, include/oxli/oxli.hh:83
+    const int k = g->k;
+    auto hash_at = [&](uint64_t r, uint64_t j) -> uint64_t {
+        const uint64_t pos = j + r * (uint64_t)(k - 1);
+        return b.hash == MURMUR ? murmur_canonical(b.bytes.data() + pos, k) : canonical2(window2(b.words.data(), pos, k), k);
+    };
+    // first position >= j in [j, e) that is NOT new (e if none)
+    auto next_old = [&](uint64_t j, uint64_t e) -> uint64_t {
+        while (j < e) {
+            uint32_t w = ~nb[j >> 5] >> (j & 31);   // old k-mers of this word from j on
+            const uint64_t wend = (j | 31) + 1;
+            if (w) {
+                const uint64_t p = j + (uint64_t)__builtin_ctz(w);
+                return p < e ? p : e;
+            }
+            j = wend;
+        }
+        return e;
+    };
     uint64_t consumed = 0;
     for (uint64_t r = 0; r < b.nreads(); r++) {
         const uint64_t a = b.koff[r], e = b.koff[r + 1];
         uint32_t since = density / 2 + 1;
-        uint64_t kmer = 0;
-        for (uint64_t j = a; j < e; j++) {
-            kmer = hashes[j];
-            const bool nw = isnew[j] != 0;
-            if (nw) {
-                ++consumed;
-                ++since;
-            } else if (g->tags.count(kmer)) {
-                since = 1;
-            } else {
-                ++since;
+        for (uint64_t j = a; j < e;) {
+            const uint64_t q = next_old(j, e);   // [j, q): new k-mers
+            if (q > j) {
+                const uint64_t t = q - j;
+                consumed += t;
+                // since + i for the i-th new k-mer (1-based); a tag at since
+                // >= density resets it to 1, so tags fall on new k-mers
+                // j + (density - since) - 1, then every density - 1 more
+                uint64_t p = since >= density ? j : j + (density - since) - 1;
+                uint64_t last_tag = ~0ull;
+                for (; p < q; p += density - 1) {
+                    g->tags.insert(hash_at(r, p));
+                    last_tag = p;
+                }
+                since = last_tag == ~0ull ? since + (uint32_t)t : (uint32_t)(q - last_tag);
+                j = q;
             }
+            if (j >= e) break;
+            // an old k-mer: a tag already resets the count
+            const uint64_t h = hash_at(r, j);
+            since = g->tags.count(h) ? 1 : since + 1;
             if (since >= density) {
-                g->tags.insert(kmer);
+                g->tags.insert(h);
                 since = 1;
             }
+            j++;
         }
         // every packed read holds >= 1 k-mer; the reference also tags the
         // (uninitialised) k-mer of reads shorter than k -- not reproduced
-        if (since >= density / 2 - 1) g->tags.insert(kmer);
+        if (e > a && since >= density / 2 - 1) g->tags.insert(hash_at(r, e - 1));
     }
     return consumed;
 }
@@ -284,11 +327,11 @@ static void consume_batch(Graph *g, const HostBatch &b, int mode, uint64_t *cons
         *consumed += b.nkmers();
         return;
     }
-    std::vector<uint8_t> isnew(b.nkmers());
-    std::vector<uint64_t> hashes(b.nkmers());
-    PassOut out{isnew.data(), hashes.data()};
+    std::vector<uint32_t> bits((b.nkmers() + 31) / 32);
+    PassOut out;
+    out.h_newbits = bits.data();
     engine_consume_host(g, b, &out);
-    *consumed += tag_batch(g, b, isnew.data(), hashes.data());
+    *consumed += tag_batch(g, b, bits.data());
 }
 
 static uint64_t batch_bases_cap(Graph *g) { return g->batch_kmers * 2 + (1u << 20); }
@@ -331,7 +374,8 @@ static void pack_raw(const RawBatch &raw, HostBatch &b, int k, int hash) {
 // starts where the previous one really ended (otherwise it parses the rest
 // of the file itself, serially).  Same reads, same order, same errors as the
 // serial parser.
-static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, uint64_t *nreads_out, uint64_t *consumed) {
+static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, uint64_t *nreads_out,
+                            uint64_t *consumed) {
     struct Chunk {
         std::vector<RawBatch> raw;
         std::vector<HostBatch> packed;
@@ -416,8 +460,7 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, uint64_t *n
                 break;
             }
             for (HostBatch &b : C.packed) {
-                if (b.nkmers()) engine_consume_host(g, b, nullptr);
-                *consumed += b.nkmers();
+                consume_batch(g, b, mode, consumed);
                 HostBatch().words.swap(b.words);
             }
             total += C.nreads;
@@ -454,8 +497,7 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, uint64_t *n
         for (const RawBatch &r : raw) {
             HostBatch b;
             pack_raw(r, b, k, hash);
-            if (b.nkmers()) engine_consume_host(g, b, nullptr);
-            *consumed += b.nkmers();
+            consume_batch(g, b, mode, consumed);
         }
         total += nr;
         if (err) {
@@ -471,10 +513,11 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, uint64_t *n
     return true;
 }
 
-static void consume_pipelined(Graph *g, Parser *parser, uint64_t *nreads_out, uint64_t *consumed) {
+// mode 0: consume (count); 1: consume and tag (consume_batch)
+static void consume_pipelined(Graph *g, Parser *parser, int mode, uint64_t *nreads_out, uint64_t *consumed) {
     if (PlainFile *pf = parser_plain_open(parser)) {
         std::unique_ptr<PlainFile, void (*)(PlainFile *)> hold(pf, parser_plain_close);
-        if (consume_chunked(g, parser, pf, nreads_out, consumed)) return;
+        if (consume_chunked(g, parser, pf, mode, nreads_out, consumed)) return;
     }
     const int T = feed_threads();
     const int npack = std::max(1, T - 1);
@@ -568,10 +611,7 @@ static void consume_pipelined(Graph *g, Parser *parser, uint64_t *nreads_out, ui
                 slots.pop_front();
                 cv.notify_all();
             }
-            if (sl->packed.nkmers()) {
-                engine_consume_host(g, sl->packed, nullptr);
-                *consumed += sl->packed.nkmers();
-            }
+            consume_batch(g, sl->packed, mode, consumed);
         }
     } catch (...) {
         finish();
@@ -594,9 +634,9 @@ int kh_consume_parser(kh_graph *h, kh_parser *ph, int mode, uint32_t *reads, uin
         std::lock_guard<std::recursive_mutex> lk(g->mu);
         KH_HIP(hipSetDevice(g->device));
         uint64_t consumed = 0, nreads = 0;
-        if (mode == 0 && feed_threads() > 1) {
+        if (feed_threads() > 1) {
             try {
-                consume_pipelined(g, ph->p, &nreads, &consumed);
+                consume_pipelined(g, ph->p, mode, &nreads, &consumed);
             } catch (...) {
                 *reads = (uint32_t)nreads;
                 *kmers = consumed;
@@ -1176,8 +1216,7 @@ int kh_graph_get_tags(kh_graph *h, uint64_t *out) {
     return guard([&] {
         CHECK_PTR(h);
         std::lock_guard<std::recursive_mutex> lk(h->g->mu);
-        std::vector<uint64_t> v(h->g->tags.begin(), h->g->tags.end());
-        std::sort(v.begin(), v.end());
+        std::vector<uint64_t> v = h->g->tags.sorted();
         memcpy(out, v.data(), v.size() * 8);
     });
 }
@@ -1196,8 +1235,7 @@ int kh_graph_save_tagset(kh_graph *h, const char *path) {
         CHECK_PTR(h);
         Graph *g = h->g;
         std::lock_guard<std::recursive_mutex> lk(g->mu);
-        std::vector<uint64_t> v(g->tags.begin(), g->tags.end());
-        std::sort(v.begin(), v.end());
+        std::vector<uint64_t> v = g->tags.sorted();
         Out o;
         o.f = fopen(path, "wb");
         if (!o.f) fail(KH_EFILE, strerror(errno));
@@ -1251,7 +1289,7 @@ int kh_graph_load_tagset(kh_graph *h, const char *path, int clear) {
             in.read(v.data() + old, m * 8);
         }
         if (clear) g->tags.clear();
-        g->tags.insert(v.begin(), v.end());
+        for (uint64_t t : v) g->tags.insert(t);
     });
 }
 

@@ -1164,7 +1164,7 @@ static void pass_stage_c(Graph *g, const Src &src, PassState &ps, const PassOut 
     hipStream_t st = g->stream;
     const uint64_t nkmers = ps.nkmers;
     const bool bigc = ps.bigc;
-    const bool want_new = out && out->h_new;
+    const bool want_new = out && (out->h_new || out->h_newbits);
     const uint64_t flag_bytes = (nkmers + 15) & ~15ull;
     uint64_t *d_out_hash = nullptr;
     if (out && out->h_hash) d_out_hash = w.rec2;  // level-2 records are dead after crossing
@@ -1178,14 +1178,16 @@ static void pass_stage_c(Graph *g, const Src &src, PassState &ps, const PassOut 
     KH_HIP(hipGetLastError());
     KH_HIP(hipMemcpyAsync(w.h_ctr, w.ctr, CTR_N * 8, hipMemcpyDeviceToHost, st));
     std::vector<uint32_t> hbits;
-    if (want_new) {
+    if (want_new && out->h_newbits) {
+        KH_HIP(hipMemcpyAsync(out->h_newbits, w.newbits, (nkmers + 31) / 32 * 4, hipMemcpyDeviceToHost, st));
+    } else if (want_new) {
         hbits.resize((nkmers + 31) / 32);
         KH_HIP(hipMemcpyAsync(hbits.data(), w.newbits, hbits.size() * 4, hipMemcpyDeviceToHost, st));
     }
     if (d_out_hash) KH_HIP(hipMemcpyAsync(out->h_hash, d_out_hash, nkmers * 8, hipMemcpyDeviceToHost, st));
     KH_HIP(hipStreamSynchronize(st));
     engine_collect_events(g);
-    if (want_new)
+    if (want_new && !out->h_newbits)
         for (uint64_t j = 0; j < nkmers; j++) out->h_new[j] = (uint8_t)((hbits[j >> 5] >> (j & 31)) & 1);
     // bigcount map overflow (a probe run too long): grow it and redo the
     // finalize of this pass (fullf and the source are intact; the map is per pass)
@@ -1234,6 +1236,10 @@ static void run_pass_small(Graph *g, const Src &src, uint64_t nkmers, const Pass
             g->bc_dirty = true;
         }
         if (out && out->h_new) out->h_new[j] = fl[j] & 1;
+        if (out && out->h_newbits) {
+            if (!(j & 31)) out->h_newbits[j >> 5] = 0;
+            out->h_newbits[j >> 5] |= (uint32_t)(fl[j] & 1) << (j & 31);
+        }
         if (out && out->h_hash) out->h_hash[j] = hs[j];
     }
 }
@@ -1246,7 +1252,7 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
         return;
     }
     PassState ps = pass_stage_a(g, src, nkmers);
-    pass_mark_local(g, ps, out && out->h_new);
+    pass_mark_local(g, ps, out && (out->h_new || out->h_newbits));
     pass_stage_c(g, src, ps, out);
 }
 
@@ -1362,6 +1368,7 @@ void engine_consume_bytes(Graph *g, const uint8_t *d_bytes, const uint64_t *d_ko
 // Passes run in stream order, so per-k-mer outputs of consecutive passes are
 // exact when each pass writes its own slice of them.
 void engine_consume_hashes(Graph *g, const uint64_t *d_hashes, uint64_t n, const PassOut *out) {
+    if (out && out->h_newbits) fail(KH_EVALUE, "hash batches report new flags per k-mer (h_new), not as a bitmap");
     const uint64_t B = std::min<uint64_t>(g->batch_kmers, MAX_PASS_KMERS);
     for (uint64_t a = 0; a < n; a += B) {
         SrcHashes s{};

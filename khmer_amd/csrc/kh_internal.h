@@ -156,6 +156,54 @@ struct Workspace {
 enum { CTR_OCC = 0, CTR_UNIQUE, CTR_NCROSS, CTR_NBC, CTR_ERR, CTR_NFULL, CTR_BCFF, CTR_BCOUT, CTR_L1Q, CTR_APQ, CTR_N };
 constexpr uint64_t BC_EMPTY = ~0ull;   // free map slot; events of hash ~0 count in CTR_BCFF
 
+// Hashgraph::all_tags (include/oxli/hashgraph.hh:113, a std::set<HashIntoType>):
+// an open-addressing set of u64 k-mer hashes (linear probing, load <= 1/2);
+// ordered output (save_tagset, get_tags) sorts on demand
+class TagSet {
+    static constexpr uint64_t EMPTY = ~0ull;
+    std::vector<uint64_t> slot_;
+    uint64_t n_ = 0;
+    bool has_empty_ = false;   // the key ~0 itself
+    static uint64_t mix(uint64_t x) {
+        x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33;
+        return x;
+    }
+    void grow() {
+        std::vector<uint64_t> old;
+        old.swap(slot_);
+        slot_.assign(old.empty() ? 1024 : old.size() * 2, EMPTY);
+        for (uint64_t x : old)
+            if (x != EMPTY) place(x);
+    }
+    void place(uint64_t x) {
+        const uint64_t m = slot_.size() - 1;
+        for (uint64_t i = mix(x) & m;; i = (i + 1) & m)
+            if (slot_[i] == EMPTY) { slot_[i] = x; return; }
+    }
+  public:
+    uint64_t size() const { return n_ + (has_empty_ ? 1 : 0); }
+    bool count(uint64_t x) const {
+        if (x == EMPTY) return has_empty_;
+        if (slot_.empty()) return false;
+        const uint64_t m = slot_.size() - 1;
+        for (uint64_t i = mix(x) & m;; i = (i + 1) & m) {
+            if (slot_[i] == x) return true;
+            if (slot_[i] == EMPTY) return false;
+        }
+    }
+    void insert(uint64_t x) {
+        if (x == EMPTY) { has_empty_ = true; return; }
+        if (2 * (n_ + 1) > slot_.size()) grow();
+        const uint64_t m = slot_.size() - 1;
+        for (uint64_t i = mix(x) & m;; i = (i + 1) & m) {
+            if (slot_[i] == x) return;
+            if (slot_[i] == EMPTY) { slot_[i] = x; n_++; return; }
+        }
+    }
+    void clear() { slot_.clear(); n_ = 0; has_empty_ = false; }
+    std::vector<uint64_t> sorted() const;   // ascending (std::set order)
+};
+
 struct Graph {
     int kind = BYTE, hash = TWOBIT, k = 0, n = 0, device = 0;
     std::vector<uint64_t> sizes, nbytes;
@@ -180,7 +228,7 @@ struct Graph {
     uint16_t *d_bc_vals = nullptr;
     uint64_t d_bc_n = 0, d_bc_cap = 0;
     bool bc_dirty = true;
-    std::unordered_set<uint64_t> tags;                  // hashgraph.hh:113 all_tags
+    TagSet tags;                                        // hashgraph.hh:113 all_tags
     uint64_t batch_kmers = 1ull << 27;
     int l2_cool = 0;                  // passes left on the exact level 2 after a capacity overflow
     // capacity margin of the fixed-capacity partition, in Poisson sigmas of
@@ -259,6 +307,7 @@ void graph_prepare_params(Graph *g);
 // into ws; copied to host by the caller).
 struct PassOut {
     uint8_t *h_new = nullptr;     // host [nkmers]
+    uint32_t *h_newbits = nullptr;   // host [(nkmers + 31) / 32]: the same flags as a bitmap (bit j & 31 of word j >> 5)
     uint64_t *h_hash = nullptr;   // host [nkmers]
 };
 void engine_consume_twobit(Graph *g, const uint64_t *d_words, const uint64_t *d_koff,

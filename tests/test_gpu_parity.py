@@ -417,3 +417,36 @@ def test_small_pass_threshold(monkeypatch, cls, small):
         vals = (ctypes.c_uint16 * max(n.value, 1))()
         check(lib.kh_graph_get_bigcounts(g._g, keys, vals, n.value, ctypes.byref(n)))
         assert dict(zip(keys[:n.value], vals[:n.value])) == o.bigcounts()
+
+
+@pytest.mark.parametrize("cls,k,chunk", [("Nodegraph", 21, 0), ("Nodegraph", 31, 20000), ("Countgraph", 25, 7001)])
+def test_tagging_genomic_multibatch(tmp_path, monkeypatch, cls, k, chunk):
+    """consume_seqfile_and_tag (src/oxli/hashgraph.cc:200-320) on a skewed
+    stream (reads of a 30 kbp genome: most k-mers are seen again, so the
+    membership test of old k-mers decides where tags fall), in several device
+    batches (tags carry from batch to batch) and, with KH_FEED_CHUNK, through
+    the chunk-parallel feed: the returned count, the tag set and the
+    .tagset bytes equal the oracle's."""
+    from khmer_amd import synth
+    if chunk:
+        monkeypatch.setenv("KH_FEED_CHUNK", str(chunk))
+    n, L = 6000, 120
+    seqs, _ = synth.genomic_batch(0, n, L, 30000)
+    fa = str(tmp_path / "g.fa")
+    with open(fa, "wb") as fh:
+        for r in range(n):
+            fh.write(b">r%d\n%s\n" % (r, seqs[r * L:(r + 1) * L]))
+    sizes = O.get_n_primes_near_x(3, 200003)
+    g, o = make_pair(cls, k, sizes)
+    from khmer_amd._lib import lib, check
+    check(lib.kh_graph_set_batch_kmers(g._g, 50000))
+    got = g.consume_seqfile_and_tag(fa)
+    want = o.consume_fastx(fa, tag=True)
+    assert got == want
+    assert sorted(g._tag_hashes()) == sorted(o.tags())
+    assert len(o.tags()) > 1000
+    assert_same(g, o, "tag")
+    f1, f2 = str(tmp_path / "g.tagset"), str(tmp_path / "o.tagset")
+    g.save_tagset(f1)
+    o.save_tagset(f2)
+    assert open(f1, "rb").read() == open(f2, "rb").read()

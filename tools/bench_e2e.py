@@ -5,6 +5,11 @@ count (src/oxli/hashtable.cc:125-150 via scripts/load-into-counting.py:143-158).
 Not the headline metric (bench.py's value is device-resident input); this is
 the PCIe/host-inclusive rate DESIGN.md reports beside it.
 
+--tag: the default load-graph.py path instead (Nodegraph.consume_seqfile_and_tag,
+src/oxli/hashgraph.cc:290-320: the device sets the bits and returns the per-k-mer
+is_new flags, the host runs the reference's per-read tag state machine),
+C3's Nodegraph k=31 4 x 4e9 unless -k / -x say otherwise.
+
 Prints one JSON line.  The FASTQ is the benchmark's synthetic stream
 (khmer_amd/synth.py), written once with fixed-width names, then read once
 untimed so it sits in the page cache.
@@ -47,12 +52,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--read-len", type=int, default=150)
-    ap.add_argument("-k", type=int, default=21)
-    ap.add_argument("-x", type=float, default=1e9)
+    ap.add_argument("-k", type=int, default=None)
+    ap.add_argument("-x", type=float, default=None)
+    ap.add_argument("--tag", action="store_true", help="Nodegraph consume_seqfile_and_tag (load-graph.py default)")
     ap.add_argument("--tables", type=int, default=4)
     ap.add_argument("--cpu-reads", type=int, default=300_000)
     ap.add_argument("--dir", default=None, help="where to write the FASTQ (default: a temporary directory)")
     a = ap.parse_args()
+    a.k = a.k or (31 if a.tag else 21)
+    a.x = a.x or (4e9 if a.tag else 1e9)
     import khmer_amd
     from khmer_amd import _lib
     _lib.set_default_device(int(os.environ.get("LOCAL_RANK", "0")))
@@ -65,15 +73,22 @@ def main():
         with open(fq, "rb") as fh:
             while fh.read(1 << 26):
                 pass
-        cg = khmer_amd.Countgraph(a.k, a.x, a.tables)
-        cg.set_use_bigcount(True)
+        def graph():
+            if a.tag:
+                return khmer_amd.Nodegraph(a.k, a.x, a.tables)
+            g = khmer_amd.Countgraph(a.k, a.x, a.tables)
+            g.set_use_bigcount(True)
+            return g
+        cg = graph()
         # warm-up: the device pipeline's first use (workspace, code objects)
         cg.consume("A" * (a.k + 10))
-        cg = khmer_amd.Countgraph(a.k, a.x, a.tables)
-        cg.set_use_bigcount(True)
+        cg = graph()
         t0 = time.perf_counter()
-        nr, nk = cg.consume_seqfile(fq)
+        nr, nk = cg.consume_seqfile_and_tag(fq) if a.tag else cg.consume_seqfile(fq)
         dt = time.perf_counter() - t0
+        n_new = None
+        if a.tag:   # consume_sequence_and_tag counts the new k-mers (src/oxli/hashgraph.cc:219-221)
+            n_new, nk = nk, a.reads * (a.read_len - a.k + 1)
         assert nr == a.reads and nk == a.reads * (a.read_len - a.k + 1), (nr, nk)
         cpu = None
         if a.cpu_reads:
@@ -83,17 +98,21 @@ def main():
             with open(sub, "rb") as fh:
                 while fh.read(1 << 26):
                     pass
-            t = O.Table(O.BYTE, a.k, cg.hashsizes())
-            t.set_use_bigcount(True)
+            t = O.Table(O.BIT if a.tag else O.BYTE, a.k, cg.hashsizes())
+            t.set_use_bigcount(not a.tag)
             t0 = time.perf_counter()
-            _, ck = t.consume_fastx(sub)
+            _, ck = t.consume_fastx(sub, tag=a.tag)
             cpu = {"value": ck / (time.perf_counter() - t0), "unit": "k-mers/s", "cores": 1, "kind": "port",
                    "sample": "%d reads of the same FASTQ layout, oracle/khmer_oracle.c consume_fastx "
                              "(parse + clean + count), 1 thread" % a.cpu_reads}
     feed = int(os.environ.get("KH_FEED_THREADS", "0")) or None
     print(json.dumps({
-        "metric": "k-mers/sec consume_seqfile end to end (page-cached FASTQ -> parse -> pack -> H2D -> count) "
-                  "into Countgraph (k=%d, %dx%.0e)" % (a.k, a.tables, a.x),
+        "metric": ("k-mers/sec consume_seqfile_and_tag end to end (page-cached FASTQ -> parse -> pack -> H2D -> "
+                   "set bits + is_new -> host tag state machine) into Nodegraph (k=%d, %dx%.0e)" if a.tag else
+                   "k-mers/sec consume_seqfile end to end (page-cached FASTQ -> parse -> pack -> H2D -> count) "
+                   "into Countgraph (k=%d, %dx%.0e)") % (a.k, a.tables, a.x),
+        "n_tags": cg.n_tags if a.tag else None,
+        "new_kmers_returned": n_new,
         "value": nk / dt, "unit": "k-mers/s", "reads": nr, "kmers": nk, "seconds": dt,
         "fastq_bytes": size, "fastq_GBps": size / dt / 1e9, "write_s": t_write,
         "host_threads": os.environ.get("OMP_NUM_THREADS"), "feed_threads_override": feed,
