@@ -359,15 +359,9 @@ static int l1f_tables_per_launch() {
     static const int v = std::max(1, std::min(L1_MAX_RPT, env_seg("KH_L1_NT", L1_MAX_RPT)));
     return v;
 }
-// threads per k_scatter_l1f workgroup: 512 (three workgroups per CU), or
-// KH_L1F_TH=1024 (one per CU, a tile of twice the records; development A/B)
-static int l1f_th() {
-    static const int v = env_seg("KH_L1F_TH", L1_THREADS) == 1024 ? 1024 : L1_THREADS;
-    return v;
-}
 static size_t lds_scatter_l1f(const Params &P, bool window, int tile_kmers) {
     const size_t F1a = (P.F1 + 3) & ~3u;
-    const size_t tile = (size_t)l1f_th() * l1f_rpt();
+    const size_t tile = (size_t)L1_THREADS * l1f_rpt();
     return F1a * 8 * 5 + (tile + 2 * F1a) * 4 + F1a * 4 * 5 + (tile + 2 * F1a) * 4 + 64 +
            lds_window(window, tile_kmers) + 2 * L1F_TW * 8;
 }
@@ -376,15 +370,14 @@ static size_t lds_scatter_l1f(const Params &P, bool window, int tile_kmers) {
 static uint32_t l1f_wpc(const Params &P) {
     static const int v = env_seg("KH_L1F_WPC", 0);
     if (v > 0) return (uint32_t)v;
-    const size_t lds = lds_scatter_l1f(P, false, l1f_th() * l1f_rpt());
-    const size_t regs = (l1f_th() == L1_THREADS ? L1F_WAVES_PER_EU : 4) * 4 / (l1f_th() / 64);
+    const size_t lds = lds_scatter_l1f(P, false, L1_THREADS * l1f_rpt());
+    const size_t regs = L1F_WAVES_PER_EU * 4 / (L1_THREADS / 64);
     return (uint32_t)std::max<size_t>(1, std::min<size_t>(regs, 163840 / lds));
 }
 static bool use_own_filter(const Graph *g);
 // workgroups of one level-1 launch over window geometry Q
 static uint32_t l1f_workgroups_q(const Graph *g, const Params &Q, uint64_t nkmers) {
-    const uint64_t th = use_own_filter(g) ? L1_THREADS : l1f_th();
-    const uint64_t tiles = (nkmers + th - 1) / th;
+    const uint64_t tiles = (nkmers + L1_THREADS - 1) / L1_THREADS;
     const uint64_t wpc = use_own_filter(g) ? 2 : l1f_wpc(Q);   // k_own_l1f: ~75 KB of LDS
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles / 8 + 1, wpc * device_cus(g)));
 }
@@ -437,33 +430,15 @@ static bool l1f_tw(const Src &src, int kpt) {
     else {
         static const bool off = env_seg("KH_L1F_TW", 1) == 0;   // development
         if (off || !src.kpr) return false;
-        const uint64_t T = (uint64_t)l1f_th() * kpt;
+        const uint64_t T = (uint64_t)L1_THREADS * kpt;
         const uint64_t reads = (T + src.kpr - 1) / src.kpr + 1;
         const uint64_t span = T + reads * (uint64_t)(src.k - 1) + (uint64_t)src.k;
         return span / 32 + 3 <= (uint64_t)L1F_TW;
     }
 }
 template <class Src>
-static L1FFn<Src> l1f_kernel(int kpt, int rpt, bool tw = false, int th = L1_THREADS) {
+static L1FFn<Src> l1f_kernel(int kpt, int rpt, bool tw = false) {
     (void)rpt;
-    if (th == 1024) {
-        if constexpr (std::is_same<Src, SrcTwoBit>::value) {
-            if (tw) {
-                switch (kpt) {
-                    case 1: return k_scatter_l1f<Src, 1, 8, true, 1024>;
-                    case 2: return k_scatter_l1f<Src, 2, 8, true, 1024>;
-                    case 4: return k_scatter_l1f<Src, 4, 8, true, 1024>;
-                    default: return k_scatter_l1f<Src, 8, 8, true, 1024>;
-                }
-            }
-        }
-        switch (kpt) {
-            case 1: return k_scatter_l1f<Src, 1, 8, false, 1024>;
-            case 2: return k_scatter_l1f<Src, 2, 8, false, 1024>;
-            case 4: return k_scatter_l1f<Src, 4, 8, false, 1024>;
-            default: return k_scatter_l1f<Src, 8, 8, false, 1024>;
-        }
-    }
     if constexpr (std::is_same<Src, SrcTwoBit>::value) {
         if (tw) {
             switch (kpt) {
@@ -782,12 +757,11 @@ static void launch_l1f(Graph *g, const Src &src, uint64_t nkmers, bool window, u
         const uint32_t nwg = l1f_workgroups_q(g, Q, nkmers);
         int kpt = 1;
         while (kpt * 2 * wn.nt <= rpt) kpt *= 2;
-        const int th = l1f_th();
-        const uint64_t tk = (uint64_t)th * kpt;
+        const uint64_t tk = (uint64_t)L1_THREADS * kpt;
         const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
         KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, g->stream));   // the chunk queue's head
-        TIMED("scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt, !window && l1f_tw(src, kpt), th), dim3(nwg),
-                                               dim3(th), lds_scatter_l1f(Q, window, (int)tk), g->stream, Q,
+        TIMED("scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt, !window && l1f_tw(src, kpt)), dim3(nwg),
+                                               dim3(L1_THREADS), lds_scatter_l1f(Q, window, (int)tk), g->stream, Q,
                                                src, nkmers, kpw, wn.t0, wn.nt, w.bkt_base + wn.bb0,
                                                (unsigned long long *)w.bkt_cur + wn.bb0, w.rec1, w.ctr, l1f_blk_sh(),
                                                jbase, l1f_chunk_tiles(g)));
@@ -1789,10 +1763,6 @@ static void set_lds_limits() {
         KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt, 8, true));
         KH_LDS_MAX(l1f_kernel<SrcBytes>(kpt, 8));
         KH_LDS_MAX(l1f_kernel<SrcHashes>(kpt, 8));
-        KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt, 8, false, 1024));
-        KH_LDS_MAX(l1f_kernel<SrcTwoBit>(kpt, 8, true, 1024));
-        KH_LDS_MAX(l1f_kernel<SrcBytes>(kpt, 8, false, 1024));
-        KH_LDS_MAX(l1f_kernel<SrcHashes>(kpt, 8, false, 1024));
     }
     KH_LDS_MAX((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>));
     for (int kpt : {1, 2, 4, 8}) {

@@ -456,22 +456,22 @@ constexpr int L1F_BLK_SH = 8;   // default block: 256 records (KH_L1F_BLK_SH)
 // LDS words per staged tile (TW) and where they live: after the kernel's
 // other arrays (lds_scatter_l1f adds 2 * L1F_TW words)
 constexpr int L1F_TW = 128;
-__host__ __device__ constexpr size_t l1f_tw_offset(size_t F1a, int rpt, int th = L1_THREADS) {
+__host__ __device__ constexpr size_t l1f_tw_offset(size_t F1a, int rpt) {
     // u64 index: 5 F1a u64 arrays, then (stage u32 + sb u16 + sj u16) per
     // record, 5 F1a u32 arrays, s_wtot, s_meta, s_koff (the window, unused
     // for fixed-length reads) rounded to 8 bytes
-    return (F1a * 8 * 5 + ((size_t)th * rpt + 2 * F1a) * 8 + F1a * 4 * 5 + 64 + 16 + 7) / 8;
+    return (F1a * 8 * 5 + ((size_t)L1_THREADS * rpt + 2 * F1a) * 8 + F1a * 4 * 5 + 64 + 16 + 7) / 8;
 }
 
-template <class Src, int KPT, int RPT_ = L1_MAX_RPT, bool TW_ = false, int TH = L1_THREADS>
-__global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_PER_EU : 4) : 4) k_scatter_l1f(Params P, Src src, uint64_t nkmers, uint64_t kpw, int t0,
+template <class Src, int KPT, int RPT_ = L1_MAX_RPT, bool TW_ = false>
+__global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) k_scatter_l1f(Params P, Src src, uint64_t nkmers, uint64_t kpw, int t0,
                                                            int nt, const uint64_t *bkt_base,
                                                            unsigned long long *bkt_cur, uint64_t *rec,
                                                            uint64_t *ctr, int blk_sh, uint32_t jbase, uint32_t cht) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int RPT = RPT_;
-    constexpr int TILE_RECS = TH * RPT;
-    constexpr int TILE_KMERS = TH * KPT;
+    constexpr int TILE_RECS = L1_THREADS * RPT;
+    constexpr int TILE_KMERS = L1_THREADS * KPT;
     const uint32_t BLK = 1u << blk_sh;
     PH_WG_BEGIN;
     constexpr uint64_t DEAD = ~0ull;
@@ -502,7 +502,7 @@ __global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_
     // window is read from there -- no per-k-mer global loads, no prefetch
     // registers
     constexpr bool TW = TW_ && std::is_same<Src, SrcTwoBit>::value;
-    uint64_t *s_tw = (uint64_t *)smem + l1f_tw_offset(F1a, RPT, TH);   // [2][L1F_TW]
+    uint64_t *s_tw = (uint64_t *)smem + l1f_tw_offset(F1a, RPT);   // [2][L1F_TW]
     const int shift = P.s0 + P.s2;
     const uint64_t omask = (1ull << shift) - 1;
     for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) {
@@ -531,7 +531,7 @@ __global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_
     if (!TW && pre) {
 #pragma unroll
         for (int a = 0; a < NPEND; a++) {
-            const uint64_t j = j0 + (uint64_t)a * TH + threadIdx.x;
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
             if (j < min(ce, j0 + TILE_KMERS)) pend[a] = kmer_fetch(src, j);
         }
     }
@@ -575,14 +575,14 @@ __global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_
         }
         // per record slot q (k-mer a = q / nt of this thread): bin offset
         // inside its bucket (~0: none) and (a << 23 | bucket << 13 | tile
-        // rank); the k-mer index is j0 + a * TH + thread: 2 VGPRs per record
+        // rank); the k-mer index is j0 + a * L1_THREADS + thread: 2 VGPRs per record
         uint32_t off[RPT], br[RPT];
 #pragma unroll
         for (int q = 0; q < RPT; q++) { off[q] = ~0u; br[q] = 0; }
         uint64_t hh[KPT];
 #pragma unroll
         for (int a = 0; a < KPT; a++) {
-            const uint64_t j = j0 + (uint64_t)a * TH + threadIdx.x;
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
             if constexpr (TW) {
                 uint64_t h = 0;
                 if (j < j1) {
@@ -599,7 +599,7 @@ __global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_
         }
 #pragma unroll
         for (int a = 0; a < KPT; a++) {
-            const uint64_t j = j0 + (uint64_t)a * TH + threadIdx.x;
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
             const bool ok = j < j1;
 #pragma unroll
             for (int q = 0; q < RPT; q++) {
@@ -618,12 +618,12 @@ __global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_
         block_sync();
         PH(1);
         // Block reservations are issued first (thread d owns bucket d and
-        // d + TH; F1 <= 1024): the returned bases are needed only
+        // d + L1_THREADS; F1 <= 1024): the returned bases are needed only
         // after the staging below, which hides the atomics' latency.
         uint64_t rsv[2] = {0, 0};
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            const uint32_t d = threadIdx.x + (uint32_t)u * TH;
+            const uint32_t d = threadIdx.x + (uint32_t)u * L1_THREADS;
             if (d < F1 && bcur[d] != DEAD) {
                 const uint32_t h = hist[d], L0 = cnt[d];
                 const uint32_t need = ((L0 + h + BLK - 1) >> blk_sh) - (((L0 + BLK - 1) & ~(BLK - 1)) >> blk_sh);
@@ -640,7 +640,7 @@ __global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_
             return h ? (h + (cnt[d] & 1u) + 1u) & ~1u : 0u;
         };
         if (F1 > 256) {
-            // many buckets: every thread scans two (F1 <= 2 * TH),
+            // many buckets: every thread scans two (F1 <= 2 * L1_THREADS),
             // wave totals through s_wtot (one more barrier)
             const uint32_t d0 = 2 * threadIdx.x;
             const uint32_t r0 = d0 < F1 ? run(d0) : 0u, r1 = d0 + 1 < F1 ? run(d0 + 1) : 0u;
@@ -686,7 +686,7 @@ __global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_
                 const uint32_t b = (br[q] >> 13) & 1023u;
                 const uint32_t pos = lstart[b] + (cnt[b] & 1u) + (br[q] & 8191u);
                 stage[pos] = off[q];
-                sbj[pos] = (b << 16) | ((br[q] >> 23) * TH + threadIdx.x);
+                sbj[pos] = (b << 16) | ((br[q] >> 23) * L1_THREADS + threadIdx.x);
             }
         }
         // The next tile's packed words go to their LDS buffer here, not after
@@ -700,7 +700,7 @@ __global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_
         if (!TW && pre) {
 #pragma unroll
             for (int a = 0; a < NPEND; a++) {
-                const uint64_t j = n0 + (uint64_t)a * TH + threadIdx.x;
+                const uint64_t j = n0 + (uint64_t)a * L1_THREADS + threadIdx.x;
                 if (j < n1 && !(KH_ABL(P, 32))) pend[a] = kmer_fetch(src, j);
             }
         }
@@ -709,7 +709,7 @@ __global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_
         // constants of this tile's run
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            const uint32_t d = threadIdx.x + (uint32_t)u * TH;
+            const uint32_t d = threadIdx.x + (uint32_t)u * L1_THREADS;
             if (d >= F1) continue;
             const uint32_t h = hist[d];
             if (!h && !last) continue;
@@ -773,12 +773,12 @@ __global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_
 #ifdef KH_L1_WO_BATCH
             // development: WU pairs per thread per step, their LDS reads issued together
             constexpr int WU = KH_L1_WO_BATCH;
-            for (uint32_t m0 = threadIdx.x; 2 * m0 < nslot; m0 += WU * TH) {
+            for (uint32_t m0 = threadIdx.x; 2 * m0 < nslot; m0 += WU * L1_THREADS) {
                 uint2 bj[WU], st[WU], ql[WU];
                 ulonglong2 dd[WU];
 #pragma unroll
                 for (int u = 0; u < WU; u++) {
-                    const uint32_t m = m0 + (uint32_t)u * TH;
+                    const uint32_t m = m0 + (uint32_t)u * L1_THREADS;
                     const bool ok = 2 * m < nslot;
                     bj[u] = ok ? sbj2[m] : make_uint2(SLOT_EMPTY, SLOT_EMPTY);
                     st[u] = ok ? stage2[m] : make_uint2(0, 0);
@@ -790,10 +790,10 @@ __global__ void __launch_bounds__(TH, TH == L1_THREADS ? (RPT_ == 8 ? L1F_WAVES_
                     dd[u] = dl2[d];
                 }
 #pragma unroll
-                for (int u = 0; u < WU; u++) put_pair(m0 + (uint32_t)u * TH, bj[u], st[u], ql[u], dd[u]);
+                for (int u = 0; u < WU; u++) put_pair(m0 + (uint32_t)u * L1_THREADS, bj[u], st[u], ql[u], dd[u]);
             }
 #else
-            for (uint32_t m = threadIdx.x; 2 * m < nslot; m += TH) {
+            for (uint32_t m = threadIdx.x; 2 * m < nslot; m += L1_THREADS) {
                 const uint2 bj = sbj2[m];
                 const uint32_t d = bj.x >> 16;
                 put_pair(m, bj, stage2[m], qq[d], dl2[d]);
