@@ -282,6 +282,19 @@ static uint64_t tag_batch(Graph *g, const HostBatch &b, const uint32_t *nb) {
         }
         return e;
     };
+    // tags are inserted in prefetched groups: the pending ones go in before
+    // any membership test (an old k-mer) and at the end of the batch
+    g->tags.reserve(g->tags.size() + b.nkmers() / (density - 1) + b.nreads() + 64);
+    uint64_t pend[64];
+    uint32_t npend = 0;
+    auto flush = [&] {
+        g->tags.insert_batch(pend, npend);
+        npend = 0;
+    };
+    auto add_tag = [&](uint64_t h) {
+        pend[npend++] = h;
+        if (npend == 64) flush();
+    };
     uint64_t consumed = 0;
     for (uint64_t r = 0; r < b.nreads(); r++) {
         const uint64_t a = b.koff[r], e = b.koff[r + 1];
@@ -297,7 +310,7 @@ static uint64_t tag_batch(Graph *g, const HostBatch &b, const uint32_t *nb) {
                 uint64_t p = since >= density ? j : j + (density - since) - 1;
                 uint64_t last_tag = ~0ull;
                 for (; p < q; p += density - 1) {
-                    g->tags.insert(hash_at(r, p));
+                    add_tag(hash_at(r, p));
                     last_tag = p;
                 }
                 since = last_tag == ~0ull ? since + (uint32_t)t : (uint32_t)(q - last_tag);
@@ -306,21 +319,89 @@ static uint64_t tag_batch(Graph *g, const HostBatch &b, const uint32_t *nb) {
             if (j >= e) break;
             // an old k-mer: a tag already resets the count
             const uint64_t h = hash_at(r, j);
+            if (npend) flush();
             since = g->tags.count(h) ? 1 : since + 1;
             if (since >= density) {
-                g->tags.insert(h);
+                add_tag(h);
                 since = 1;
             }
             j++;
         }
         // every packed read holds >= 1 k-mer; the reference also tags the
         // (uninitialised) k-mer of reads shorter than k -- not reproduced
-        if (e > a && since >= density / 2 - 1) g->tags.insert(hash_at(r, e - 1));
+        if (e > a && since >= density / 2 - 1) add_tag(hash_at(r, e - 1));
     }
+    flush();
     return consumed;
 }
 
-static void consume_batch(Graph *g, const HostBatch &b, int mode, uint64_t *consumed) {
+// The tag state machine of a consume_seqfile_and_tag call runs on its own
+// host thread, batch by batch in stream order, while the calling thread
+// already feeds the next batch to the device (the device pass needs no tag
+// state).  Only that thread touches the tag set until finish().
+struct TagPipe {
+    Graph *g;
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::pair<HostBatch, std::vector<uint32_t>>> q;
+    bool done = false;
+    std::exception_ptr err;
+    uint64_t consumed = 0;
+    explicit TagPipe(Graph *g_) : g(g_) {
+        th = std::thread([this] {
+            for (;;) {
+                std::pair<HostBatch, std::vector<uint32_t>> job;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return done || !q.empty(); });
+                    if (q.empty()) return;
+                    job = std::move(q.front());
+                    q.pop_front();
+                    cv.notify_all();
+                }
+                try {
+                    if (!err) consumed += tag_batch(g, job.first, job.second.data());
+                } catch (...) {
+                    err = std::current_exception();
+                }
+            }
+        });
+    }
+    // at most two batches wait (bounded host memory)
+    void push(HostBatch &&b, std::vector<uint32_t> &&bits) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return q.size() < 2; });
+        q.emplace_back(std::move(b), std::move(bits));
+        cv.notify_all();
+    }
+    // every pushed batch tagged; the tagged k-mer count, or the tagger's error
+    uint64_t finish() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            done = true;
+            cv.notify_all();
+        }
+        if (th.joinable()) th.join();
+        if (err) std::rethrow_exception(err);
+        return consumed;
+    }
+    ~TagPipe() {
+        if (th.joinable()) {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                done = true;
+                cv.notify_all();
+            }
+            th.join();
+        }
+    }
+};
+static thread_local TagPipe *t_tagpipe = nullptr;   // set by kh_consume_parser (mode 1)
+
+// mode 0: count; 1: count and tag (through t_tagpipe when set: the batch is
+// moved to the tagger, so callers must not use it afterwards)
+static void consume_batch(Graph *g, HostBatch &b, int mode, uint64_t *consumed) {
     if (b.nkmers() == 0) return;
     if (mode == 0) {
         engine_consume_host(g, b, nullptr);
@@ -331,7 +412,8 @@ static void consume_batch(Graph *g, const HostBatch &b, int mode, uint64_t *cons
     PassOut out;
     out.h_newbits = bits.data();
     engine_consume_host(g, b, &out);
-    *consumed += tag_batch(g, b, bits.data());
+    if (t_tagpipe) t_tagpipe->push(std::move(b), std::move(bits));
+    else *consumed += tag_batch(g, b, bits.data());
 }
 
 static uint64_t batch_bases_cap(Graph *g) { return g->batch_kmers * 2 + (1u << 20); }
@@ -635,13 +717,20 @@ int kh_consume_parser(kh_graph *h, kh_parser *ph, int mode, uint32_t *reads, uin
         KH_HIP(hipSetDevice(g->device));
         uint64_t consumed = 0, nreads = 0;
         if (feed_threads() > 1) {
+            std::unique_ptr<TagPipe> tp(mode == 1 ? new TagPipe(g) : nullptr);
+            t_tagpipe = tp.get();
             try {
                 consume_pipelined(g, ph->p, mode, &nreads, &consumed);
             } catch (...) {
+                t_tagpipe = nullptr;
+                // the reads before the error are consumed and tagged
+                if (tp) consumed += tp->finish();
                 *reads = (uint32_t)nreads;
                 *kmers = consumed;
                 throw;
             }
+            t_tagpipe = nullptr;
+            if (tp) consumed += tp->finish();
             *reads = (uint32_t)nreads;
             *kmers = consumed;
             return;

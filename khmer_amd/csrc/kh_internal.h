@@ -168,13 +168,14 @@ class TagSet {
         x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33;
         return x;
     }
-    void grow() {
+    void rehash(uint64_t cap) {
         std::vector<uint64_t> old;
         old.swap(slot_);
-        slot_.assign(old.empty() ? 1024 : old.size() * 2, EMPTY);
+        slot_.assign(cap, EMPTY);
         for (uint64_t x : old)
             if (x != EMPTY) place(x);
     }
+    void grow() { rehash(slot_.empty() ? 1024 : slot_.size() * 2); }
     void place(uint64_t x) {
         const uint64_t m = slot_.size() - 1;
         for (uint64_t i = mix(x) & m;; i = (i + 1) & m)
@@ -201,6 +202,20 @@ class TagSet {
         }
     }
     void clear() { slot_.clear(); n_ = 0; has_empty_ = false; }
+    // capacity for n keys at load <= 1/2 (one rehash instead of a doubling chain)
+    void reserve(uint64_t n) {
+        uint64_t c = 1024;
+        while (c < 2 * n) c *= 2;
+        if (c > slot_.size()) rehash(c);
+    }
+    // n inserts with their slots prefetched first: the table is far larger
+    // than the caches, so one-at-a-time inserts wait on a miss each
+    void insert_batch(const uint64_t *x, uint64_t n) {
+        reserve(n_ + n);
+        const uint64_t m = slot_.size() - 1;
+        for (uint64_t a = 0; a < n; a++) __builtin_prefetch(&slot_[mix(x[a]) & m], 1);
+        for (uint64_t a = 0; a < n; a++) insert(x[a]);
+    }
     std::vector<uint64_t> sorted() const;   // ascending (std::set order)
 };
 

@@ -10,4 +10,4 @@ mkdir -p "$out"
 T="timeout -k 10 300"
 $T python3 tools/loopback_bench.py 8 25000000 1 1677721600 1 1e9 > "$out/lb_g8_exchange_c2.json" 2> "$out/lb.err" && tail -1 "$out/lb_g8_exchange_c2.json" &&
 $T python3 tools/loopback_bench.py 8 25000000 1 1677721600 0 1e9 > "$out/lb_g8_broadcast_c2.json" 2>> "$out/lb.err" && tail -1 "$out/lb_g8_broadcast_c2.json" &&
-$T python3 tools/loopback_bench.py 8 25000000 1 1677721600 1 8e9 > "$out/lb_g8_exchange_c4.json" 2>> "$out/lb.err" && tail -1 "$out/lb_g8_exchange_c4.json" || { tail -20 "$out/lb.err"; exit 1; }
+$T python3 tools/loopback_bench.py 8 12500000 1 838860800 1 8e9 > "$out/lb_g8_exchange_c4.json" 2>> "$out/lb.err" && tail -1 "$out/lb_g8_exchange_c4.json" || { tail -20 "$out/lb.err"; exit 1; }
