@@ -362,10 +362,17 @@ def main():
     else:
         runner = SingleGpuBench(args, local, sizes)
 
+    def progress(what):   # stderr, outside the timed region: long multi-rank runs show life
+        if rank == 0:
+            sys.stderr.write("bench.py: %s\n" % what)
+            sys.stderr.flush()
+
     runner.setup()
+    progress("setup done")
     for _ in range(args.warmup):
         runner.step()
     runner.sync()
+    progress("warmup done")
     runner.barrier()
     runner.profile(True)
     t0 = time.perf_counter()
@@ -375,6 +382,7 @@ def main():
     t1 = time.perf_counter()
     runner.barrier()
     elapsed = runner.max_over_ranks(t1 - t0)
+    progress("timed steps done")
     stats = runner.kernel_stats()
     runner.profile(False)
     # the same K steps again without the per-kernel HIP events: how much the
@@ -402,6 +410,7 @@ def main():
                 check_info.update(q)
         fx = None
     if fx is not None:
+        progress("hashing the tables for the %s check" % fx["config"])
         sha = runner.table_sha256()   # collective when sharded
         if rank == 0:
             check_info.update(compare_fixture(fx, check_info["n_unique_kmers"], check_info["n_occupied"], sha,

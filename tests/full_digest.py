@@ -32,6 +32,10 @@ CONFIGS = {
     # skewed ("genomic") stream, 2 Mbp genome at ~750x: saturation + heavy bigcount
     "genomic_c2": dict(kind=1, hash=0, k=21, n=4, x=1e9, reads=10_000_000, L=150, bigcount=True,
                        genome=2_000_000, batch_kmers=1 << 29),
+    # BASELINE C4's tables at a read count a multi-rank dry run through the host
+    # transport (tools/r4_dry.sh) moves in minutes
+    "c4_400k": dict(kind=1, hash=0, k=21, n=4, x=8e9, reads=400_000, L=150, bigcount=True,
+                    genome=0, batch_kmers=1 << 28),
     # C5 query geometry with counts that spread over 1..15 and saturate (VERDICT
     # r3 "Next round" #3): 4 x 8e9 nibbles, genomic streams at ~8x k-mer coverage
     "c5_genomic": dict(kind=7, hash=0, k=31, n=4, x=8e9, reads=4_000_000, L=150, bigcount=False,
@@ -51,6 +55,7 @@ EXCHANGE = {
     "genomic_c2_x2": ("genomic_c2", 2, 1 << 29),
     "c4_shape_x2": ("c4_shape", 2, 1 << 28),
     "c4_shape_x8": ("c4_shape", 8, 1 << 28),
+    "c4_400k_x2": ("c4_400k", 2, 3200 << 20),     # bench.py --gpus 2 --config C4 --strong --reads 400000
     "c5m_shape_x2": ("c5m_shape", 2, 1 << 26),
     "c5m_shape_x8": ("c5m_shape", 8, 1 << 26),
     "c5m_genomic_x2": ("c5m_genomic", 2, 1 << 26),
