@@ -27,6 +27,12 @@
 // inside a compressed block (truncated .gz / .bz2) or carries corrupt data
 // raises KH_EFILE (OSError), as the reference's tests expect
 // (tests/test_read_parsers.py:183-255).
+//
+// Decompression runs off the parsing thread: BGZF files (chains of
+// independent gzip members, htslib's bgzip format) are inflated member group
+// by member group on worker threads, every other compressed stream on one
+// read-ahead thread; either way the parser sees the same bytes in the same
+// order, and a corrupt stream raises after the bytes before the damage.
 #include <ctype.h>
 #include <stdio.h>
 #include <string.h>
@@ -37,8 +43,10 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <memory>
 #include <string>
+#include <thread>
 
 #include "kh_internal.h"
 
@@ -152,6 +160,248 @@ struct MemSource : Source {
     }
 };
 
+// Worker threads for decompression: the job's CPU share (OMP_NUM_THREADS,
+// as the feed's packers) halved, 2..8; KH_INFLATE_THREADS overrides.
+int inflate_threads() {
+    int n = (int)std::thread::hardware_concurrency();
+    const char *e = getenv("OMP_NUM_THREADS");
+    if (e && atoi(e) > 0) n = std::min(n > 0 ? n : 1, atoi(e));
+    n = std::max(2, std::min(8, n / 2));
+    const char *f = getenv("KH_INFLATE_THREADS");
+    if (f && atoi(f) > 0) n = std::min(64, atoi(f));
+    return n;
+}
+
+// Decompressed bytes handed over in file order through a ring of R slots:
+// producers fill slot g % R with group g once group g - R has been read.
+// A producer that meets damage stores the bytes it could decode and the
+// error; the consumer returns those bytes, then raises.
+struct RingSource : Source {
+    struct Slot {
+        std::vector<unsigned char> out;
+        size_t len = 0, pos = 0;
+        bool ready = false, last = false;
+        std::string err;   // the complete message (KH_EFILE) raised after the bytes
+    };
+    std::vector<Slot> ring;
+    std::mutex mu;
+    std::condition_variable cv_free, cv_ready;
+    uint64_t cur = 0;        // the group the consumer reads
+    bool stop = false, ended = false;
+    std::vector<std::thread> th;
+
+    void start_ring(int R) { ring.resize((size_t)R); }
+    void stop_threads() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv_free.notify_all();
+        for (auto &t : th) t.join();
+        th.clear();
+    }
+    // producer side: wait until group g's slot is free (false: stopping)
+    bool wait_free(uint64_t g) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_free.wait(lk, [&] { return stop || g < cur + ring.size(); });
+        return !stop;
+    }
+    void publish(uint64_t g) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            ring[g % ring.size()].ready = true;
+        }
+        cv_ready.notify_all();
+    }
+    size_t read(unsigned char *dst, size_t n) override {
+        for (;;) {
+            if (ended) return 0;
+            Slot &s = ring[cur % ring.size()];
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv_ready.wait(lk, [&] { return s.ready; });
+            }
+            if (s.pos < s.len) {
+                const size_t k = std::min(n, s.len - s.pos);
+                memcpy(dst, s.out.data() + s.pos, k);
+                s.pos += k;
+                return k;
+            }
+            if (!s.err.empty()) fail(KH_EFILE, s.err);
+            if (s.last) { ended = true; return 0; }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                s.ready = false;
+                s.pos = s.len = 0;
+                cur++;
+            }
+            cv_free.notify_all();
+        }
+    }
+};
+
+// BGZF (SAM/BAM format specification 4.1): gzip members with FLG.FEXTRA whose
+// 'BC' subfield holds the member size - 1, each inflating to <= 64 KiB.  The
+// whole file is checked to be such a chain up front (headers only); a file
+// that is not (one member, other flags, a truncated tail) takes zlib's gzread
+// path instead, so its bytes and errors are zlib's.
+struct BgzfSource : RingSource {
+    struct Member { uint64_t cdata; uint32_t clen, crc, isize; };
+    int fd = -1;
+    const unsigned char *p = nullptr;
+    size_t n = 0;
+    std::vector<Member> mem;
+    std::vector<size_t> gfirst;   // group g = members [gfirst[g], gfirst[g + 1])
+    uint64_t next_g = 0;          // next group a worker takes (under mu)
+    static constexpr size_t GROUP = 64;   // members per group (<= 4 MiB)
+
+    ~BgzfSource() override {
+        stop_threads();
+        if (p) munmap((void *)p, n);
+        if (fd >= 0) close(fd);
+    }
+    static uint32_t le32(const unsigned char *q) {
+        return (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
+    }
+    bool scan() {
+        size_t off = 0;
+        while (off < n) {
+            const unsigned char *h = p + off;
+            if (n - off < 12 + 6 + 8 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 4) return false;
+            const size_t xlen = (size_t)h[10] | (size_t)h[11] << 8;
+            if (off + 12 + xlen > n) return false;
+            long bsize = -1;
+            for (size_t x = 12; x + 4 <= 12 + xlen;) {
+                const size_t slen = (size_t)h[x + 2] | (size_t)h[x + 3] << 8;
+                if (h[x] == 'B' && h[x + 1] == 'C' && slen == 2 && x + 6 <= 12 + xlen)
+                    bsize = (long)h[x + 4] | (long)h[x + 5] << 8;
+                x += 4 + slen;
+            }
+            if (bsize < 0) return false;
+            const size_t total = (size_t)bsize + 1;
+            if (total < 12 + xlen + 8 || off + total > n) return false;
+            Member m;
+            m.cdata = off + 12 + xlen;
+            m.clen = (uint32_t)(total - 12 - xlen - 8);
+            m.crc = le32(h + total - 8);
+            m.isize = le32(h + total - 4);
+            if (m.isize > 65536) return false;
+            mem.push_back(m);
+            off += total;
+        }
+        return mem.size() >= 2;
+    }
+    void worker() {
+        z_stream z;
+        memset(&z, 0, sizeof z);
+        if (inflateInit2(&z, -15) != Z_OK) return;
+        for (;;) {
+            uint64_t g;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                if (stop || next_g + 1 >= gfirst.size()) break;
+                g = next_g++;
+            }
+            if (!wait_free(g)) break;
+            Slot &s = ring[g % ring.size()];
+            size_t need = 0;
+            for (size_t i = gfirst[g]; i < gfirst[g + 1]; i++) need += mem[i].isize;
+            if (s.out.size() < need) s.out.resize(need);
+            size_t len = 0;
+            std::string err;
+            for (size_t i = gfirst[g]; i < gfirst[g + 1] && err.empty(); i++) {
+                const Member &m = mem[i];
+                inflateReset(&z);
+                z.next_in = (Bytef *)(p + m.cdata);
+                z.avail_in = m.clen;
+                z.next_out = s.out.data() + len;
+                z.avail_out = m.isize;
+                const int rc = inflate(&z, Z_FINISH);
+                const size_t got = m.isize - z.avail_out;
+                if (rc != Z_STREAM_END) {
+                    err = z.msg ? z.msg : (rc == Z_BUF_ERROR ? "incorrect length check" : "invalid compressed data");
+                } else if (z.avail_in != 0 || got != m.isize) {
+                    err = "incorrect length check";
+                } else if (crc32(0, s.out.data() + len, (uInt)got) != m.crc) {
+                    err = "incorrect data check";
+                }
+                len += got;
+            }
+            s.len = len;
+            s.pos = 0;
+            s.err = err.empty() ? err : "File " + path + ": " + err;
+            s.last = g + 2 == gfirst.size() || !err.empty();
+            publish(g);
+            if (!err.empty()) break;   // nothing after the damage is read
+        }
+        inflateEnd(&z);
+    }
+    bool open(const char *path_) {
+        path = path_;
+        fd = ::open(path_, O_RDONLY);
+        if (fd < 0) return false;
+        struct stat st;
+        if (fstat(fd, &st) != 0 || st.st_size < (1 << 20)) return false;   // small files: zlib
+        n = (size_t)st.st_size;
+        void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) { m = nullptr; n = 0; return false; }
+        p = (const unsigned char *)m;
+        madvise(m, n, MADV_SEQUENTIAL);
+        if (!scan()) return false;
+        for (size_t i = 0; i < mem.size(); i += GROUP) gfirst.push_back(i);
+        gfirst.push_back(mem.size());
+        const int nw = inflate_threads();
+        start_ring(2 * nw);
+        for (int t = 0; t < nw; t++) th.emplace_back([this] { worker(); });
+        return true;
+    }
+};
+
+// Any other compressed stream: the inner source (zlib gzread, libbz2) runs
+// on one thread that fills 4 MiB slots ahead of the parser.
+struct ReadAheadSource : RingSource {
+    std::unique_ptr<Source> in;
+    static constexpr size_t CHUNK = 4 << 20;
+    ~ReadAheadSource() override { stop_threads(); }
+    void producer() {
+        for (uint64_t g = 0;; g++) {
+            if (!wait_free(g)) return;
+            Slot &s = ring[g % ring.size()];
+            if (s.out.size() < CHUNK) s.out.resize(CHUNK);
+            size_t len = 0;
+            bool end = false;
+            std::string err;
+            try {
+                while (len < CHUNK) {
+                    const size_t k = in->read(s.out.data() + len, CHUNK - len);
+                    if (k == 0) { end = true; break; }
+                    len += k;
+                }
+            } catch (const std::exception &e) {   // the inner source's "File <path>: ..."
+                err = e.what();
+                if (err.empty()) err = "File " + path + ": read error";
+            }
+            s.len = len;
+            s.pos = 0;
+            s.err = err;
+            s.last = end || !err.empty();
+            publish(g);
+            if (s.last) return;
+        }
+    }
+    void begin(std::unique_ptr<Source> inner) {
+        in = std::move(inner);
+        path = in->path;
+        start_ring(3);
+        th.emplace_back([this] { producer(); });
+    }
+};
+
+static bool async_off() {
+    static const bool v = [] { const char *e = getenv("KH_ASYNC_INFLATE"); return e && atoi(e) == 0; }();
+    return v;
+}
+
 std::unique_ptr<Source> open_source(const char *path) {
     unsigned char magic[3] = {0, 0, 0};
     FILE *f = fopen(path, "rb");
@@ -163,16 +413,27 @@ std::unique_ptr<Source> open_source(const char *path) {
         b->path = path;
         b->f = f;
         b->start();
-        return std::move(b);
+        if (async_off()) return std::move(b);
+        std::unique_ptr<ReadAheadSource> r(new ReadAheadSource());
+        r->begin(std::move(b));
+        return std::move(r);
     }
     fclose(f);
+    const bool gzip_magic = m == 3 && magic[0] == 0x1f && magic[1] == 0x8b;
+    if (gzip_magic && !async_off()) {
+        std::unique_ptr<BgzfSource> bg(new BgzfSource());
+        if (bg->open(path)) return std::move(bg);
+    }
     gzFile gz = gzopen(path, "rb");
     if (!gz) return nullptr;
     gzbuffer(gz, 1 << 20);
     std::unique_ptr<GzSource> g(new GzSource());
     g->path = path;
     g->gz = gz;
-    return std::move(g);
+    if (g->plain() || async_off()) return std::move(g);
+    std::unique_ptr<ReadAheadSource> r(new ReadAheadSource());
+    r->begin(std::move(g));
+    return std::move(r);
 }
 }  // namespace
 

@@ -220,3 +220,113 @@ def test_no_device_graph_raises():
         pytest.skip("device present")
     with pytest.raises(RuntimeError):
         khmer.Countgraph(21, 1e5, 4)
+
+
+# ---- compressed input off the parsing thread (kh_parser.cpp BgzfSource /
+# ReadAheadSource): same records and errors as the serial zlib path ----
+
+def _plain_25k(tmp_path):
+    import gzip
+    raw = gzip.decompress(open(data("25k.fq.gz"), "rb").read())
+    f = tmp_path / "25k.fq"
+    f.write_bytes(raw)
+    return raw, str(f)
+
+
+def _records(path):
+    return [(r.name, r.sequence, r.quality) for r in khmer.ReadParser(path)]
+
+
+def test_parser_bgzf(tmp_path):
+    """A BGZF file (worker-thread inflate of member groups) parses to the
+    oracle's records of the plain file; Python's gzip reads the same bytes."""
+    import gzip
+    from tests import bgzf
+    raw, plain = _plain_25k(tmp_path)
+    blob = bgzf.compress(raw)
+    assert gzip.decompress(blob) == raw and len(bgzf.member_offsets(blob)) > 32
+    f = tmp_path / "25k.fq.bgz"
+    f.write_bytes(blob)
+    ours = _records(str(f))
+    assert len(ours) == 25000
+    assert ours == list(O.read_fastx(plain))
+
+
+def test_parser_bgzf_small_members(tmp_path):
+    """Members of a few hundred bytes: records cross many member and group
+    boundaries."""
+    from tests import bgzf
+    raw, plain = _plain_25k(tmp_path)
+    f = tmp_path / "small.fq.gz"
+    f.write_bytes(bgzf.compress(raw, block=777))
+    assert _records(str(f)) == list(O.read_fastx(plain))
+
+
+@pytest.mark.parametrize("where", ["member", "crc"])
+def test_parser_bgzf_corrupt(tmp_path, where):
+    """Damage in a middle member: OSError, after exactly the records that lie
+    wholly before that member's group (never a record past the damage)."""
+    from tests import bgzf
+    raw, plain = _plain_25k(tmp_path)
+    blob = bytearray(bgzf.compress(raw))
+    offs = bgzf.member_offsets(bytes(blob))
+    i = len(offs) // 2
+    if where == "member":
+        blob[offs[i] + 40] ^= 0xFF              # inside the deflate data
+    else:
+        blob[offs[i + 1] - 8] ^= 0x01           # the member's CRC32
+    f = tmp_path / "bad.fq.gz"
+    f.write_bytes(bytes(blob))
+    ours = []
+    with pytest.raises(OSError):
+        for r in khmer.ReadParser(str(f)):
+            ours.append((r.name, r.sequence, r.quality))
+    theirs = list(O.read_fastx(plain))
+    assert 0 < len(ours) < len(theirs) and ours == theirs[:len(ours)]
+    # the records returned end inside the damaged member (its bytes decoded
+    # before the damage is found), and every earlier member's records came
+    end = 0
+    for _ in range(4 * len(ours)):
+        end = raw.index(b"\n", end) + 1
+    assert i * 65280 - 1000 <= end <= (i + 1) * 65280
+
+
+def test_parser_bgzf_truncated(tmp_path):
+    """A BGZF file cut inside a member is not a clean chain: zlib's path
+    (read-ahead thread), OSError after a prefix of the records."""
+    from tests import bgzf
+    raw, plain = _plain_25k(tmp_path)
+    blob = bgzf.compress(raw)
+    f = tmp_path / "cut.fq.gz"
+    f.write_bytes(blob[:len(blob) // 2 + 123])
+    ours = []
+    with pytest.raises(OSError):
+        for r in khmer.ReadParser(str(f)):
+            ours.append((r.name, r.sequence, r.quality))
+    theirs = list(O.read_fastx(plain))
+    assert 0 < len(ours) < len(theirs) and ours == theirs[:len(ours)]
+
+
+def test_parser_multimember_gzip(tmp_path):
+    """Concatenated plain gzip members (no BC field): the zlib path reads
+    them all, as gzread does."""
+    import gzip
+    raw, plain = _plain_25k(tmp_path)
+    cut = raw.index(b"\n@", len(raw) // 3) + 1
+    f = tmp_path / "cat.fq.gz"
+    f.write_bytes(gzip.compress(raw[:cut]) + gzip.compress(raw[cut:]))
+    assert _records(str(f)) == list(O.read_fastx(plain))
+
+
+def test_parser_gzip_closed_early(tmp_path):
+    """A parser closed after one read (decompression still running ahead)
+    shuts its threads down."""
+    from tests import bgzf
+    raw, _ = _plain_25k(tmp_path)
+    f = tmp_path / "early.fq.gz"
+    f.write_bytes(bgzf.compress(raw))
+    for path in (str(f), data("25k.fq.gz")):
+        for _ in range(20):
+            p = khmer.ReadParser(path)
+            next(iter(p))
+            del p

@@ -98,3 +98,39 @@ def test_chunked_feed_parser_object(monkeypatch):
     reads, kmers = g.consume_seqfile(rp)
     assert rp.num_reads == reads == 99
     assert g.consume_seqfile(rp) == (0, 0)
+
+
+@pytest.mark.parametrize("how", ["bgzf", "gzip", "bz2"])
+def test_compressed_feed_matches_plain(tmp_path, monkeypatch, how):
+    """Compressed input (BGZF member groups inflated on worker threads, other
+    gzip / bzip2 streams on a read-ahead thread) consumes to exactly the
+    plain file's tables and counters."""
+    import bz2
+    import gzip
+    from tests import bgzf
+    plain = str(tmp_path / "in.fq")
+    _write_fastq(plain, 40000)
+    raw = open(plain, "rb").read()
+    blob = {"bgzf": lambda: bgzf.compress(raw, block=8192), "gzip": lambda: gzip.compress(raw),
+            "bz2": lambda: bz2.compress(raw)}[how]()
+    if how == "bgzf":
+        assert len(blob) > (1 << 20)   # large enough for the worker-thread path
+    comp = str(tmp_path / ("in.fq." + how))
+    open(comp, "wb").write(blob)
+    want = _consume(monkeypatch, plain, 1 << 30, 1)
+    assert _consume(monkeypatch, comp, 1 << 30, 8) == want
+    assert want[0] == (40000, 40000 * 100)
+
+
+def test_bgzf_feed_corrupt_member(tmp_path, monkeypatch):
+    """A damaged BGZF member: consume_seqfile raises OSError."""
+    from tests import bgzf
+    plain = str(tmp_path / "in.fq")
+    _write_fastq(plain, 40000)
+    blob = bytearray(bgzf.compress(open(plain, "rb").read(), block=8192))
+    offs = bgzf.member_offsets(bytes(blob))
+    blob[offs[len(offs) // 2] + 30] ^= 0xFF
+    comp = str(tmp_path / "bad.fq.gz")
+    open(comp, "wb").write(bytes(blob))
+    rk, err, _, _, _ = _consume(monkeypatch, comp, 1 << 30, 8)
+    assert rk is None and err[0] is OSError

@@ -5,6 +5,11 @@ count (src/oxli/hashtable.cc:125-150 via scripts/load-into-counting.py:143-158).
 Not the headline metric (bench.py's value is device-resident input); this is
 the PCIe/host-inclusive rate DESIGN.md reports beside it.
 
+--compress gzip|bgzf: the same FASTQ gzip-compressed (one member, zlib level
+6) or BGZF-compressed (htslib's bgzip layout, tests/bgzf.py; members
+compressed on a thread pool here), to time the compressed-input feed
+(KH_ASYNC_INFLATE=0 selects the serial inflate for an A/B).
+
 --tag: the default load-graph.py path instead (Nodegraph.consume_seqfile_and_tag,
 src/oxli/hashgraph.cc:290-320: the device sets the bits and returns the per-k-mer
 is_new flags, the host runs the reference's per-read tag state machine),
@@ -48,6 +53,48 @@ def write_fastq(path, nreads, L, chunk=1_000_000):
             fh.write(out.tobytes())
 
 
+def _bgzf_part(args):
+    from tests import bgzf
+    raw, block = args
+    return b"".join(bgzf.member(raw[i:i + block]) for i in range(0, len(raw), block))
+
+
+def compress(fq, how):
+    """The FASTQ at fq compressed as `how` (the plain file is removed)."""
+    if how == "none":
+        return fq
+    import zlib
+    out = fq + (".gz" if how == "gzip" else ".bgz")
+    with open(fq, "rb") as src, open(out, "wb") as dst:
+        if how == "gzip":
+            z = zlib.compressobj(6, zlib.DEFLATED, 31)
+            while True:
+                b = src.read(1 << 24)
+                if not b:
+                    break
+                dst.write(z.compress(b))
+            dst.write(z.flush())
+        else:
+            from multiprocessing.pool import ThreadPool   # zlib releases the GIL
+            from tests import bgzf
+            block, span = 65280, 65280 * 64
+            with ThreadPool(min(16, os.cpu_count() or 1)) as pool:
+                def spans():
+                    while True:
+                        b = src.read(span)
+                        if not b:
+                            return
+                        yield b, block
+                for part in pool.imap(_bgzf_part, spans(), chunksize=4):
+                    dst.write(part)
+            dst.write(bgzf.member(b""))
+    os.remove(fq)
+    with open(out, "rb") as fh:
+        while fh.read(1 << 26):
+            pass
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=10_000_000)
@@ -57,18 +104,39 @@ def main():
     ap.add_argument("--tag", action="store_true", help="Nodegraph consume_seqfile_and_tag (load-graph.py default)")
     ap.add_argument("--tables", type=int, default=4)
     ap.add_argument("--cpu-reads", type=int, default=300_000)
+    ap.add_argument("--compress", choices=["none", "gzip", "bgzf"], default="none")
+    ap.add_argument("--make", default=None, help="only write the (compressed) FASTQ to this path and exit")
+    ap.add_argument("--input", default=None, help="time this file (written by --make with the same --reads)")
     ap.add_argument("--dir", default=None, help="where to write the FASTQ (default: a temporary directory)")
     a = ap.parse_args()
+    if a.make:
+        write_fastq(a.make, a.reads, a.read_len)
+        fq_bytes = os.path.getsize(a.make)
+        t0 = time.perf_counter()
+        out = compress(a.make, a.compress)
+        print(json.dumps({"made": out, "fastq_bytes": fq_bytes, "file_bytes": os.path.getsize(out),
+                          "compress_s": time.perf_counter() - t0}), flush=True)
+        return
     a.k = a.k or (31 if a.tag else 21)
     a.x = a.x or (4e9 if a.tag else 1e9)
     import khmer_amd
     from khmer_amd import _lib
     _lib.set_default_device(int(os.environ.get("LOCAL_RANK", "0")))
     with tempfile.TemporaryDirectory(dir=a.dir) as tmp:
-        fq = os.path.join(tmp, "reads.fq")
-        t0 = time.perf_counter()
-        write_fastq(fq, a.reads, a.read_len)
-        t_write = time.perf_counter() - t0
+        if a.input:
+            fq, t_write, t_compress = a.input, 0.0, 0.0
+            w = len(str(a.reads))
+            fq_bytes = a.reads * (2 * a.read_len + 7 + w)
+            a.compress = {".gz": "gzip", ".bgz": "bgzf"}.get(os.path.splitext(fq)[1], "none")
+        else:
+            fq = os.path.join(tmp, "reads.fq")
+            t0 = time.perf_counter()
+            write_fastq(fq, a.reads, a.read_len)
+            t_write = time.perf_counter() - t0
+            fq_bytes = os.path.getsize(fq)
+            t0 = time.perf_counter()
+            fq = compress(fq, a.compress)
+            t_compress = time.perf_counter() - t0
         size = os.path.getsize(fq)
         with open(fq, "rb") as fh:
             while fh.read(1 << 26):
@@ -114,7 +182,9 @@ def main():
         "n_tags": cg.n_tags if a.tag else None,
         "new_kmers_returned": n_new,
         "value": nk / dt, "unit": "k-mers/s", "reads": nr, "kmers": nk, "seconds": dt,
-        "fastq_bytes": size, "fastq_GBps": size / dt / 1e9, "write_s": t_write,
+        "compress": a.compress, "async_inflate": os.environ.get("KH_ASYNC_INFLATE", "1") != "0",
+        "file_bytes": size, "file_GBps": size / dt / 1e9, "fastq_bytes": fq_bytes, "fastq_GBps": fq_bytes / dt / 1e9,
+        "write_s": t_write, "compress_s": t_compress,
         "host_threads": os.environ.get("OMP_NUM_THREADS"), "feed_threads_override": feed,
         "n_unique_kmers": cg.n_unique_kmers(), "n_occupied": cg.n_occupied(),
         "cpu_baseline": cpu,
