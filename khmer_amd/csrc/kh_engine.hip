@@ -374,6 +374,15 @@ static uint32_t l1f_wpc(const Params &P) {
     const size_t regs = L1F_WAVES_PER_EU * 4 / (L1_THREADS / 64);
     return (uint32_t)std::max<size_t>(1, std::min<size_t>(regs, 163840 / lds));
 }
+// A 2-bit (or ASCII) source's level 1 in one k_scatter_l1f launch needs
+// all F1 buckets' LDS arrays: beyond ~590 buckets only one workgroup fits a
+// CU, and the exact two-pass level 1 is faster there (C3, 956 buckets: 404
+// against 475 ms/step, profiles/r4/c3_level1.txt).  KH_L1F_ONE_WG=1 keeps the
+// one-workgroup launch (development A/B).
+static bool l1f_direct(const Params &P) {
+    static const bool one = env_seg("KH_L1F_ONE_WG", 0) != 0;
+    return P.F1 <= 1024 && (one || l1f_wpc(P) >= 2);
+}
 static bool use_own_filter(const Graph *g);
 // workgroups of one level-1 launch over window geometry Q
 static uint32_t l1f_workgroups_q(const Graph *g, const Params &Q, uint64_t nkmers) {
@@ -1020,7 +1029,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
     bool l1f = false;
     uint64_t nrec = 0;   // records this pass writes (exact level 1 only)
     for (;;) {
-        l1f = fast && l1f_ok(g) && (std::is_same<Src, SrcHashes>::value || P.F1 <= 1024);
+        l1f = fast && l1f_ok(g) && (std::is_same<Src, SrcHashes>::value || l1f_direct(P));
         const bool ownf = fast && !window && use_own_filter(g) && own_l1f_on();
         const uint64_t cap1 = (l1f || ownf) ? bkt_plan(g, nkmers) : 0;
         // level 1
@@ -2400,9 +2409,10 @@ static void a2a_level1(Graph *V, const Src &src, uint64_t nkmers, uint32_t jbase
     const PassGeo q = pass_geo(P, nkmers);
     ws_prepare(V, q);
     const uint64_t F1 = P.F1;
-    w.l1_exact = !std::is_same<Src, SrcHashes>::value && P.F1 > 1024;
+    w.l1_exact = !std::is_same<Src, SrcHashes>::value && !l1f_direct(P);
     if (w.l1_exact) {
-        // more than 1024 buckets (C4 / C5 tables): the exact two-pass level 1
+        // more buckets than one fast launch holds at two workgroups per CU
+        // (C3 / C4 / C5 tables): the exact two-pass level 1
         // (as pass_stage_a) -- bucket b's records are [off1[b], off1[b + 1])
         KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
         TIMED_G(V, "hist_l1", hipLaunchKernelGGL(k_hist_l1<Src>, dim3(q.nch1), dim3(L1_THREADS),
