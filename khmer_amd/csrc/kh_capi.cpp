@@ -17,6 +17,7 @@
 #include <deque>
 #include <exception>
 #include <string>
+#include <functional>
 #include <thread>
 
 #include "../../include/khmer_hip.h"
@@ -37,7 +38,11 @@ struct PlainFile;
 PlainFile *parser_plain_open(Parser *pr);
 void parser_plain_close(PlainFile *f);
 size_t plain_size(const PlainFile *f);
-size_t plain_record_start(const PlainFile *f, size_t from, size_t limit);
+bool plain_chunkable(const PlainFile *f, size_t CH);
+void plain_parse_chunk(const PlainFile *f, size_t c, size_t CH, int k, uint64_t max_kmers, std::vector<RawBatch> &out,
+                       uint64_t *nreads, size_t *start, size_t *end, bool *redo);
+void plain_parse_rest(const PlainFile *f, size_t from, size_t CH, int k, uint64_t max_kmers,
+                      const std::function<void(RawBatch &)> &sink, uint64_t *nreads);
 uint64_t plain_parse_range(const PlainFile *f, size_t start, size_t stop, int k, uint64_t max_kmers,
                            std::vector<RawBatch> &out, uint64_t *nreads);
 void parser_mark_drained(Parser *pr, uint64_t nreads);
@@ -450,20 +455,22 @@ static void pack_raw(const RawBatch &raw, HostBatch &b, int k, int hash) {
     }
 }
 
-// Chunk-parallel feed of a plain file (kh_parser.cpp parser_plain_open):
-// worker threads parse and pack chunks of ~64 MB cut at record starts; the
-// calling thread consumes them in file order after checking that each chunk
-// starts where the previous one really ended (otherwise it parses the rest
-// of the file itself, serially).  Same reads, same order, same errors as the
+// Chunk-parallel feed of a plain or BGZF file (kh_parser.cpp
+// parser_plain_open): worker threads parse and pack chunks of ~64 MB of the
+// (inflated) stream cut at record starts; the calling thread consumes them in
+// file order after checking that each chunk starts where the previous one
+// really ended and could be parsed on its own (otherwise it parses the rest
+// of the input itself, serially).  Same reads, same order, same errors as the
 // serial parser.
 static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, uint64_t *nreads_out,
                             uint64_t *consumed) {
     struct Chunk {
         std::vector<RawBatch> raw;
         std::vector<HostBatch> packed;
-        uint64_t nreads = 0, start = 0, end = 0;
+        uint64_t nreads = 0;
+        size_t start = 0, end = 0;
         std::exception_ptr err;
-        bool ready = false;
+        bool ready = false, redo = false;
     };
     const size_t n = plain_size(pf);
     const char *ce = getenv("KH_FEED_CHUNK");   // development / tests: chunk bytes
@@ -471,7 +478,7 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
     const size_t nch = (n + CH - 1) / CH;
     // no recognisable record start inside the second chunk (CRLF or wrapped
     // FASTQ): the streaming reader/packer pipeline instead
-    if (nch > 1 && plain_record_start(pf, CH, CH) >= n) return false;
+    if (nch > 1 && !plain_chunkable(pf, CH)) return false;
     const int T = std::max(1, feed_threads() - 1);
     const size_t depth = (size_t)T * 2;
     const uint64_t maxk = std::min<uint64_t>(g->batch_kmers, 1ull << 27);
@@ -495,17 +502,7 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
                 }
                 Chunk &C = *ch[c];
                 try {
-                    // a chunk without a recognised record start parses nothing
-                    // (the consumer then continues serially); a chunk whose
-                    // successor has none stops at the first record boundary
-                    // past its own end, so no chunk holds much more than CH
-                    C.start = plain_record_start(pf, c * CH, CH);
-                    size_t stop_at = n;
-                    if (c + 1 < nch) {
-                        stop_at = plain_record_start(pf, (c + 1) * CH, CH);
-                        if (stop_at >= n) stop_at = (c + 1) * CH;
-                    }
-                    C.end = C.start < n ? plain_parse_range(pf, C.start, stop_at, k, maxk, C.raw, &C.nreads) : n;
+                    plain_parse_chunk(pf, c, CH, k, maxk, C.raw, &C.nreads, &C.start, &C.end, &C.redo);
                 } catch (...) {
                     C.err = std::current_exception();
                 }
@@ -537,7 +534,9 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
                 cv.wait(lk, [&] { return ch[c]->ready; });
             }
             Chunk &C = *ch[c];
-            if (C.start != true_end && !(C.start >= n && true_end >= n)) {   // a chunk start that was not a record start
+            // a chunk start that was not a record start, or a chunk that could
+            // not be parsed on its own
+            if (C.redo || (C.start != true_end && !(C.start >= n && true_end >= n))) {
                 serial_rest = true;
                 break;
             }
@@ -564,31 +563,19 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
         throw;
     }
     finish();
-    // the rest of the file serially, in pieces of about CH bytes (each piece
-    // ends on a real record boundary), so host memory stays bounded
-    while (serial_rest && true_end < n) {
-        std::vector<RawBatch> raw;
-        uint64_t nr = 0;
-        std::exception_ptr err;
-        size_t end = n;
+    // the rest of the input serially
+    if (serial_rest && true_end < n) {
         try {
-            end = plain_parse_range(pf, true_end, std::min(n, true_end + CH), k, maxk, raw, &nr);
+            plain_parse_rest(pf, true_end, CH, k, maxk, [&](RawBatch &r) {
+                HostBatch b;
+                pack_raw(r, b, k, hash);
+                consume_batch(g, b, mode, consumed);
+            }, &total);
         } catch (...) {
-            err = std::current_exception();
-        }
-        for (const RawBatch &r : raw) {
-            HostBatch b;
-            pack_raw(r, b, k, hash);
-            consume_batch(g, b, mode, consumed);
-        }
-        total += nr;
-        if (err) {
             *nreads_out = total;
             parser_mark_drained(parser, total);
-            std::rethrow_exception(err);
+            throw;
         }
-        if (end <= true_end) break;   // no progress: end of input
-        true_end = end;
     }
     *nreads_out = total;
     parser_mark_drained(parser, total);

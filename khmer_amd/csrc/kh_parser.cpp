@@ -44,6 +44,7 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <functional>
 #include <memory>
 #include <string>
 #include <thread>
@@ -245,12 +246,88 @@ struct RingSource : Source {
 // whole file is checked to be such a chain up front (headers only); a file
 // that is not (one member, other flags, a truncated tail) takes zlib's gzread
 // path instead, so its bytes and errors are zlib's.
+struct BgzfMember { uint64_t cdata; uint32_t clen, crc, isize; };
+
+static uint32_t le32(const unsigned char *q) {
+    return (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
+}
+bool bgzf_scan(const unsigned char *p, size_t n, std::vector<BgzfMember> &mem) {
+    size_t off = 0;
+    while (off < n) {
+        const unsigned char *h = p + off;
+        if (n - off < 12 + 6 + 8 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 4) return false;
+        const size_t xlen = (size_t)h[10] | (size_t)h[11] << 8;
+        if (off + 12 + xlen > n) return false;
+        long bsize = -1;
+        for (size_t x = 12; x + 4 <= 12 + xlen;) {
+            const size_t slen = (size_t)h[x + 2] | (size_t)h[x + 3] << 8;
+            if (h[x] == 'B' && h[x + 1] == 'C' && slen == 2 && x + 6 <= 12 + xlen)
+                bsize = (long)h[x + 4] | (long)h[x + 5] << 8;
+            x += 4 + slen;
+        }
+        if (bsize < 0) return false;
+        const size_t total = (size_t)bsize + 1;
+        if (total < 12 + xlen + 8 || off + total > n) return false;
+        BgzfMember m;
+        m.cdata = off + 12 + xlen;
+        m.clen = (uint32_t)(total - 12 - xlen - 8);
+        m.crc = le32(h + total - 8);
+        m.isize = le32(h + total - 4);
+        if (m.isize > 65536) return false;
+        mem.push_back(m);
+        off += total;
+    }
+    return mem.size() >= 2;
+}
+// inflate member m of the mapped file p into dst (m.isize bytes of room):
+// the bytes decoded (all of them, or those before the damage) and, on
+// damage, zlib's message in *err
+size_t bgzf_inflate(z_stream &z, const unsigned char *p, const BgzfMember &m, unsigned char *dst, std::string *err) {
+    inflateReset(&z);
+    z.next_in = (Bytef *)(p + m.cdata);
+    z.avail_in = m.clen;
+    z.next_out = dst;
+    z.avail_out = m.isize;
+    const int rc = inflate(&z, Z_FINISH);
+    const size_t got = m.isize - z.avail_out;
+    if (rc != Z_STREAM_END)
+        *err = z.msg ? z.msg : (rc == Z_BUF_ERROR ? "incorrect length check" : "invalid compressed data");
+    else if (z.avail_in != 0 || got != m.isize)
+        *err = "incorrect length check";
+    else if (crc32(0, dst, (uInt)got) != m.crc)
+        *err = "incorrect data check";
+    return got;
+}
+// a raw-deflate decoder for bgzf_inflate
+struct Inflater {
+    z_stream z;
+    bool ok = false;
+    Inflater() {
+        memset(&z, 0, sizeof z);
+        ok = inflateInit2(&z, -15) == Z_OK;
+    }
+    ~Inflater() { if (ok) inflateEnd(&z); }
+};
+// a read-only mapping of a whole file
+bool map_file(const char *path, int *fd, const unsigned char **p, size_t *n, size_t min_size) {
+    *fd = ::open(path, O_RDONLY);
+    if (*fd < 0) return false;
+    struct stat st;
+    if (fstat(*fd, &st) != 0 || st.st_size <= 0 || (size_t)st.st_size < min_size) return false;
+    void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, *fd, 0);
+    if (m == MAP_FAILED) return false;
+    *p = (const unsigned char *)m;
+    *n = (size_t)st.st_size;
+    madvise(m, *n, MADV_SEQUENTIAL);
+    return true;
+}
+
+// The BGZF stream, member groups inflated by worker threads into the ring.
 struct BgzfSource : RingSource {
-    struct Member { uint64_t cdata; uint32_t clen, crc, isize; };
     int fd = -1;
     const unsigned char *p = nullptr;
     size_t n = 0;
-    std::vector<Member> mem;
+    std::vector<BgzfMember> mem;
     std::vector<size_t> gfirst;   // group g = members [gfirst[g], gfirst[g + 1])
     uint64_t next_g = 0;          // next group a worker takes (under mu)
     static constexpr size_t GROUP = 64;   // members per group (<= 4 MiB)
@@ -260,41 +337,9 @@ struct BgzfSource : RingSource {
         if (p) munmap((void *)p, n);
         if (fd >= 0) close(fd);
     }
-    static uint32_t le32(const unsigned char *q) {
-        return (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
-    }
-    bool scan() {
-        size_t off = 0;
-        while (off < n) {
-            const unsigned char *h = p + off;
-            if (n - off < 12 + 6 + 8 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 4) return false;
-            const size_t xlen = (size_t)h[10] | (size_t)h[11] << 8;
-            if (off + 12 + xlen > n) return false;
-            long bsize = -1;
-            for (size_t x = 12; x + 4 <= 12 + xlen;) {
-                const size_t slen = (size_t)h[x + 2] | (size_t)h[x + 3] << 8;
-                if (h[x] == 'B' && h[x + 1] == 'C' && slen == 2 && x + 6 <= 12 + xlen)
-                    bsize = (long)h[x + 4] | (long)h[x + 5] << 8;
-                x += 4 + slen;
-            }
-            if (bsize < 0) return false;
-            const size_t total = (size_t)bsize + 1;
-            if (total < 12 + xlen + 8 || off + total > n) return false;
-            Member m;
-            m.cdata = off + 12 + xlen;
-            m.clen = (uint32_t)(total - 12 - xlen - 8);
-            m.crc = le32(h + total - 8);
-            m.isize = le32(h + total - 4);
-            if (m.isize > 65536) return false;
-            mem.push_back(m);
-            off += total;
-        }
-        return mem.size() >= 2;
-    }
     void worker() {
-        z_stream z;
-        memset(&z, 0, sizeof z);
-        if (inflateInit2(&z, -15) != Z_OK) return;
+        Inflater inf;
+        if (!inf.ok) return;
         for (;;) {
             uint64_t g;
             {
@@ -309,24 +354,8 @@ struct BgzfSource : RingSource {
             if (s.out.size() < need) s.out.resize(need);
             size_t len = 0;
             std::string err;
-            for (size_t i = gfirst[g]; i < gfirst[g + 1] && err.empty(); i++) {
-                const Member &m = mem[i];
-                inflateReset(&z);
-                z.next_in = (Bytef *)(p + m.cdata);
-                z.avail_in = m.clen;
-                z.next_out = s.out.data() + len;
-                z.avail_out = m.isize;
-                const int rc = inflate(&z, Z_FINISH);
-                const size_t got = m.isize - z.avail_out;
-                if (rc != Z_STREAM_END) {
-                    err = z.msg ? z.msg : (rc == Z_BUF_ERROR ? "incorrect length check" : "invalid compressed data");
-                } else if (z.avail_in != 0 || got != m.isize) {
-                    err = "incorrect length check";
-                } else if (crc32(0, s.out.data() + len, (uInt)got) != m.crc) {
-                    err = "incorrect data check";
-                }
-                len += got;
-            }
+            for (size_t i = gfirst[g]; i < gfirst[g + 1] && err.empty(); i++)
+                len += bgzf_inflate(inf.z, p, mem[i], s.out.data() + len, &err);
             s.len = len;
             s.pos = 0;
             s.err = err.empty() ? err : "File " + path + ": " + err;
@@ -334,20 +363,14 @@ struct BgzfSource : RingSource {
             publish(g);
             if (!err.empty()) break;   // nothing after the damage is read
         }
-        inflateEnd(&z);
     }
     bool open(const char *path_) {
         path = path_;
-        fd = ::open(path_, O_RDONLY);
-        if (fd < 0) return false;
-        struct stat st;
-        if (fstat(fd, &st) != 0 || st.st_size < (1 << 20)) return false;   // small files: zlib
-        n = (size_t)st.st_size;
-        void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
-        if (m == MAP_FAILED) { m = nullptr; n = 0; return false; }
-        p = (const unsigned char *)m;
-        madvise(m, n, MADV_SEQUENTIAL);
-        if (!scan()) return false;
+        // small files: zlib (KH_BGZF_MIN_BYTES: development / tests)
+        const char *e = getenv("KH_BGZF_MIN_BYTES");
+        const size_t min_bytes = e ? (size_t)atoll(e) : (size_t)1 << 20;
+        if (!map_file(path_, &fd, &p, &n, std::max<size_t>(1, min_bytes))) return false;
+        if (!bgzf_scan(p, n, mem)) return false;
         for (size_t i = 0; i < mem.size(); i += GROUP) gfirst.push_back(i);
         gfirst.push_back(mem.size());
         const int nw = inflate_threads();
@@ -629,61 +652,114 @@ void parser_fill_batch(Parser *p, HostBatch &b, int k, uint64_t max_kmers, uint6
     }
 }
 
-// ---- chunk-parallel parsing of plain files (kh_capi.cpp consume_pipelined) ----
-// A plain FASTA/FASTQ file that no read has been taken from yet is mapped and
-// cut into chunks at record starts; each chunk is parsed by its own Parser
-// over the mapped bytes (the same record semantics), so parsing scales with
+// ---- chunk-parallel parsing (kh_capi.cpp consume_chunked) ----
+// A plain FASTA/FASTQ file, or a BGZF file, that no read has been taken from
+// yet is cut into chunks at record starts; each chunk is parsed by its own
+// Parser over its bytes (the same record semantics), so parsing scales with
 // threads.  A chunk start is a line beginning with '>' (FASTA: unambiguous) or
 // with '@' that begins two consecutive well-formed four-line records (FASTQ).
 // Chunk c's parser stops at the first record boundary at or past chunk c+1's
 // start; the consumer checks that they coincide and otherwise re-parses the
-// rest of the file serially from where chunk c really ended (exact either way).
+// rest of the input serially from where chunk c really ended (exact either
+// way).  A plain file is mapped whole.  A BGZF file is a stream of known
+// length (the members' ISIZE) whose members can be inflated independently:
+// chunk c inflates only the members under its window, [c*CH - 1, (c+1)*CH +
+// BGZF_EXTRA); a record that runs past the window, or damage inside it,
+// makes the chunk "redo" and the consumer continues serially from there
+// through a sequential member reader (the streaming source's bytes, order and
+// errors).
 struct PlainFile {
     std::string path;
     int fd = -1;
-    const unsigned char *p = nullptr;
-    size_t n = 0;
+    const unsigned char *p = nullptr;   // the mapped file
+    size_t mapped = 0;
+    size_t n = 0;                        // stream bytes (BGZF: inflated)
     bool fastq = false;
+    bool bgzf = false;
+    std::vector<BgzfMember> mem;         // BGZF members
+    std::vector<uint64_t> uoff;          // BGZF: stream offset of member i (size + 1)
     ~PlainFile() {
-        if (p) munmap((void *)p, n);
+        if (p) munmap((void *)p, mapped);
         if (fd >= 0) close(fd);
     }
 };
 
+constexpr size_t BGZF_LIM = 1 << 20;     // record-start search span in a BGZF window
+constexpr size_t BGZF_EXTRA = 4 << 20;   // window bytes past the chunk's end
+
+// bytes [lo, hi) of an n-byte stream, b[0] being byte lo
+struct View {
+    const unsigned char *b;
+    size_t lo, hi, n;
+};
+
+static bool chunk_bgzf_on() {
+    const char *e = getenv("KH_BGZF_CHUNKED");   // development / tests: 0 streams BGZF through one parser
+    return !(e && atoi(e) == 0);
+}
+
 PlainFile *parser_plain_open(Parser *pr) {
     std::lock_guard<std::mutex> lk(pr->mu);
-    if (pr->num_reads != 0 || pr->offset() != 0 || !pr->broken.empty() || !pr->src->plain()) return nullptr;
+    if (pr->num_reads != 0 || pr->offset() != 0 || !pr->broken.empty()) return nullptr;
+    const bool bg = dynamic_cast<BgzfSource *>(pr->src.get()) != nullptr;
+    if (!pr->src->plain() && !(bg && chunk_bgzf_on())) return nullptr;
     std::unique_ptr<PlainFile> f(new PlainFile());
     f->path = pr->path;
     f->fastq = pr->fastq;
-    f->fd = open(pr->path.c_str(), O_RDONLY);
-    if (f->fd < 0) return nullptr;
-    struct stat st;
-    if (fstat(f->fd, &st) != 0 || st.st_size <= 0) return nullptr;
-    f->n = (size_t)st.st_size;
-    void *m = mmap(nullptr, f->n, PROT_READ, MAP_PRIVATE, f->fd, 0);
-    if (m == MAP_FAILED) return nullptr;
-    f->p = (const unsigned char *)m;
-    madvise(m, f->n, MADV_SEQUENTIAL);
+    if (!map_file(pr->path.c_str(), &f->fd, &f->p, &f->mapped, 1)) return nullptr;
+    f->n = f->mapped;
+    if (bg) {
+        if (!bgzf_scan(f->p, f->mapped, f->mem)) return nullptr;
+        f->bgzf = true;
+        f->uoff.resize(f->mem.size() + 1);
+        f->uoff[0] = 0;
+        for (size_t i = 0; i < f->mem.size(); i++) f->uoff[i + 1] = f->uoff[i] + f->mem[i].isize;
+        f->n = f->uoff.back();
+    }
     return f.release();
 }
 void parser_plain_close(PlainFile *f) { delete f; }
 size_t plain_size(const PlainFile *f) { return f->n; }
 
-// the first record start in [from, from + limit) (f->n if none there): the
+// first member whose bytes reach past offset x
+static size_t bgzf_member_at(const PlainFile *f, size_t x) {
+    return (size_t)(std::upper_bound(f->uoff.begin(), f->uoff.end(), (uint64_t)x) - f->uoff.begin()) - 1;
+}
+// inflate the members under stream bytes [lo, hi) into buf; the view covers
+// whole members; false on damage
+static bool bgzf_window(const PlainFile *f, size_t lo, size_t hi, std::vector<unsigned char> &buf, View *v) {
+    const size_t ma = bgzf_member_at(f, lo);
+    size_t mb = ma;
+    while (mb < f->mem.size() && f->uoff[mb] < hi) mb++;
+    buf.resize((size_t)(f->uoff[mb] - f->uoff[ma]));
+    Inflater inf;
+    if (!inf.ok) return false;
+    size_t len = 0;
+    for (size_t i = ma; i < mb; i++) {
+        std::string err;
+        len += bgzf_inflate(inf.z, f->p, f->mem[i], buf.data() + len, &err);
+        if (!err.empty()) return false;
+    }
+    *v = View{buf.data(), (size_t)f->uoff[ma], (size_t)f->uoff[mb], f->n};
+    return true;
+}
+static View whole(const PlainFile *f) { return View{f->p, 0, f->n, f->n}; }
+
+// the first record start in [from, from + limit) (v.n if none there): the
 // search is bounded, so a file whose records the heuristic cannot recognise
-// (CRLF or line-wrapped FASTQ) costs each chunk at most `limit` bytes of scan
-size_t plain_record_start(const PlainFile *f, size_t from, size_t limit) {
-    const unsigned char *p = f->p, *e = f->p + f->n;
+// (CRLF or line-wrapped FASTQ) costs each chunk at most `limit` bytes of scan.
+// Needs from - 1 >= v.lo.
+static size_t record_start(const View &v, bool fastq, size_t from, size_t limit) {
     if (from == 0) return 0;
-    if (from >= f->n) return f->n;
-    const unsigned char *lim = limit < f->n - from ? p + from + limit : e;
-    auto line_end = [&](const unsigned char *q) -> const unsigned char * {
-        const void *x = memchr(q, '\n', (size_t)(e - q));
-        return x ? (const unsigned char *)x : e;
+    if (from >= v.n || from >= v.hi) return v.n;
+    const unsigned char *B = v.b, *e = v.b + (v.hi - v.lo);
+    const unsigned char *q = B + (from - v.lo);
+    const unsigned char *lim = limit < v.hi - from ? q + limit : e;
+    auto line_end = [&](const unsigned char *x) -> const unsigned char * {
+        const void *m = memchr(x, '\n', (size_t)(e - x));
+        return m ? (const unsigned char *)m : e;
     };
     // start of the first line beginning at or after from
-    const unsigned char *q = p + from;
     if (q[-1] != '\n') {
         q = line_end(q);
         if (q < e) q++;
@@ -708,55 +784,221 @@ size_t plain_record_start(const PlainFile *f, size_t from, size_t limit) {
         return true;
     };
     while (q < lim) {
-        if (!f->fastq) {
-            if (*q == '>') return (size_t)(q - p);
+        if (!fastq) {
+            if (*q == '>') return v.lo + (size_t)(q - B);
         } else if (*q == '@') {
             const unsigned char *n1, *n2;
-            if (record4(q, &n1) && (n1 >= e || record4(n1, &n2))) return (size_t)(q - p);
+            if (record4(q, &n1) && (n1 >= e || record4(n1, &n2))) return v.lo + (size_t)(q - B);
         }
         q = line_end(q);
         if (q < e) q++;
     }
-    return f->n;
+    return v.n;
+}
+size_t plain_record_start(const PlainFile *f, size_t from, size_t limit) {
+    return record_start(whole(f), f->fastq, from, limit);
+}
+
+// a chunk parser over stream bytes from `start` (same record rules as the
+// file's own parser; the first-read rule was settled by the file's first record)
+static void chunk_parser(Parser &pr, const PlainFile *f, const unsigned char *p, size_t nbytes) {
+    std::unique_ptr<MemSource> ms(new MemSource());
+    ms->path = f->path;
+    ms->p = p;
+    ms->n = nbytes;
+    ms->pos = 0;
+    pr.src = std::move(ms);
+    pr.path = f->path;
+    pr.buf.resize(1 << 22);
+    pr.fastq = f->fastq;
+    pr.have_qualities = f->fastq;
+    pr.num_reads = 1;
+}
+static void add_raw(std::vector<RawBatch> &out, const std::string &seq, int k, uint64_t max_kmers) {
+    const size_t n = seq.size();
+    if (n < (size_t)k) return;
+    RawBatch *b = &out.back();
+    if (b->nkmers >= max_kmers) {
+        out.emplace_back();
+        b = &out.back();
+    }
+    b->seq.insert(b->seq.end(), seq.begin(), seq.end());
+    b->len.push_back((uint32_t)n);
+    b->nkmers += n - (size_t)k + 1;
+    b->nreads_parsed++;
 }
 
 // Parse records starting at byte `start` until the next record would start at
 // or past `stop`; returns the offset where parsing stopped.  Reads >= k bases
 // go into raw batches of <= max_kmers k-mers (out grows by one batch at a
 // time).  *nreads counts good reads; a malformed record throws after the
-// reads before it are in out.
+// reads before it are in out.  *overrun: the parse needed bytes past the
+// view that the stream has (its result is void; nothing thrown).
+static uint64_t parse_range(const View &v, const PlainFile *f, size_t start, size_t stop, int k, uint64_t max_kmers,
+                            std::vector<RawBatch> &out, uint64_t *nreads, bool *overrun) {
+    Parser pr;
+    chunk_parser(pr, f, v.b + (start - v.lo), v.hi - start);
+    if (out.empty()) out.emplace_back();
+    *overrun = false;
+    try {
+        for (;;) {
+            if (start + pr.offset() >= stop) break;
+            if (pr.next_read_locked() == KH_END) break;
+            (*nreads)++;
+            add_raw(out, pr.seq, k, max_kmers);
+        }
+    } catch (...) {
+        if (pr.eof && v.hi < v.n) { *overrun = true; return start + pr.offset(); }
+        throw;
+    }
+    if (pr.eof && v.hi < v.n) *overrun = true;
+    return start + pr.offset();
+}
 uint64_t plain_parse_range(const PlainFile *f, size_t start, size_t stop, int k, uint64_t max_kmers,
                            std::vector<RawBatch> &out, uint64_t *nreads) {
+    bool overrun;
+    return parse_range(whole(f), f, start, stop, k, max_kmers, out, nreads, &overrun);
+}
+
+// Is a chunked parse worth starting (a record start recognised inside the
+// second chunk)?  Single-chunk inputs always are.
+bool plain_chunkable(const PlainFile *f, size_t CH) {
+    if (f->n <= CH) return true;
+    if (!f->bgzf) return record_start(whole(f), f->fastq, CH, CH) < f->n;
+    std::vector<unsigned char> buf;
+    View v;
+    if (!bgzf_window(f, CH - 1, std::min(f->n, CH + BGZF_EXTRA), buf, &v)) return false;
+    return record_start(v, f->fastq, CH, BGZF_LIM) < f->n;
+}
+
+// Chunk c of CH bytes: where its first record starts (n: none recognised),
+// where its parse really ended, its reads; *redo: the chunk could not be
+// parsed on its own (the consumer continues serially from its start).  A
+// malformed record throws after the reads before it are in out.
+void plain_parse_chunk(const PlainFile *f, size_t c, size_t CH, int k, uint64_t max_kmers, std::vector<RawBatch> &out,
+                       uint64_t *nreads, size_t *start, size_t *end, bool *redo) {
+    const size_t n = f->n, nch = (n + CH - 1) / CH;
+    *redo = false;
+    std::vector<unsigned char> buf;
+    View v = whole(f);
+    size_t lim = CH;
+    if (f->bgzf) {
+        lim = BGZF_LIM;
+        const size_t lo = c ? c * CH - 1 : 0, hi = std::min(n, (c + 1) * CH + BGZF_EXTRA);
+        if (!bgzf_window(f, lo, hi, buf, &v)) {   // damage: the serial rest meets it in order
+            *start = *end = n;
+            *redo = true;
+            return;
+        }
+    }
+    // a chunk without a recognised record start parses nothing (the consumer
+    // then continues serially); a chunk whose successor has none stops at the
+    // first record boundary past its own end, so no chunk holds much more than CH
+    *start = record_start(v, f->fastq, c * CH, lim);
+    size_t stop_at = n;
+    if (c + 1 < nch) {
+        stop_at = record_start(v, f->fastq, (c + 1) * CH, lim);
+        if (stop_at >= n) stop_at = (c + 1) * CH;
+    }
+    *end = n;
+    if (*start < n) {
+        bool overrun = false;
+        *end = parse_range(v, f, *start, stop_at, k, max_kmers, out, nreads, &overrun);
+        if (overrun) {
+            out.clear();
+            *nreads = 0;
+            *redo = true;
+        }
+    }
+}
+
+// BGZF members in order from stream offset `from` (the streaming source's
+// bytes, with its damage messages), for the serial rest
+struct BgzfSeqSource : Source {
+    const PlainFile *f;
+    size_t m, skip;
+    Inflater inf;
+    std::vector<unsigned char> buf = std::vector<unsigned char>(65536);
+    size_t pos = 0, len = 0;
+    std::string err;
+    size_t read(unsigned char *dst, size_t want) override {
+        while (pos >= len) {
+            if (!err.empty()) fail(KH_EFILE, "File " + path + ": " + err);
+            if (m >= f->mem.size()) return 0;
+            len = bgzf_inflate(inf.z, f->p, f->mem[m++], buf.data(), &err);
+            pos = std::min(skip, len);
+            skip -= pos;
+        }
+        const size_t k = std::min(want, len - pos);
+        memcpy(dst, buf.data() + pos, k);
+        pos += k;
+        return k;
+    }
+};
+
+// The rest of the input from `from`, serially, batch by batch to sink; *nreads
+// counts the reads parsed (a malformed record or damage throws after the
+// reads before it are sunk and counted).
+void plain_parse_rest(const PlainFile *f, size_t from, size_t CH, int k, uint64_t max_kmers,
+                      const std::function<void(RawBatch &)> &sink, uint64_t *nreads) {
+    if (!f->bgzf) {
+        // in pieces of about CH bytes (each piece ends on a real record
+        // boundary), so host memory stays bounded
+        while (from < f->n) {
+            std::vector<RawBatch> raw;
+            uint64_t nr = 0;
+            std::exception_ptr err;
+            size_t end = f->n;
+            try {
+                end = plain_parse_range(f, from, std::min(f->n, from + CH), k, max_kmers, raw, &nr);
+            } catch (...) {
+                err = std::current_exception();
+            }
+            for (RawBatch &r : raw) sink(r);
+            *nreads += nr;
+            if (err) std::rethrow_exception(err);
+            if (end <= from) break;   // no progress: end of input
+            from = end;
+        }
+        return;
+    }
+    if (from >= f->n) return;
     Parser pr;
-    std::unique_ptr<MemSource> ms(new MemSource());
-    ms->path = f->path;
-    ms->p = f->p;
-    ms->n = f->n;
-    ms->pos = start;
-    pr.src = std::move(ms);
+    std::unique_ptr<BgzfSeqSource> src(new BgzfSeqSource());
+    src->path = f->path;
+    src->f = f;
+    src->m = bgzf_member_at(f, from);
+    src->skip = from - (size_t)f->uoff[src->m];
+    pr.src = std::move(src);
     pr.path = f->path;
     pr.buf.resize(1 << 22);
     pr.fastq = f->fastq;
     pr.have_qualities = f->fastq;
-    pr.num_reads = 1;   // the first-read rule (have_qualities) was settled by the file's first record
-    if (out.empty()) out.emplace_back();
+    pr.num_reads = 1;
     for (;;) {
-        if (start + pr.offset() >= stop) break;
-        if (pr.next_read_locked() == KH_END) break;
-        (*nreads)++;
-        const size_t n = pr.seq.size();
-        if (n < (size_t)k) continue;
-        RawBatch *b = &out.back();
-        if (b->nkmers >= max_kmers) {
-            out.emplace_back();
-            b = &out.back();
+        RawBatch b;
+        std::exception_ptr err;
+        bool done = false;
+        uint64_t nr = 0;
+        try {
+            while (b.nkmers < max_kmers) {
+                if (pr.next_read_locked() == KH_END) { done = true; break; }
+                nr++;
+                b.nreads_parsed++;
+                const size_t n = pr.seq.size();
+                if (n < (size_t)k) continue;
+                b.seq.insert(b.seq.end(), pr.seq.begin(), pr.seq.end());
+                b.len.push_back((uint32_t)n);
+                b.nkmers += n - (size_t)k + 1;
+            }
+        } catch (...) {
+            err = std::current_exception();
         }
-        b->seq.insert(b->seq.end(), pr.seq.begin(), pr.seq.end());
-        b->len.push_back((uint32_t)n);
-        b->nkmers += n - (size_t)k + 1;
-        b->nreads_parsed++;
+        sink(b);
+        *nreads += nr;
+        if (err) std::rethrow_exception(err);
+        if (done) return;
     }
-    return start + pr.offset();
 }
 
 // the parser has been drained by the chunk path: reads counted, nothing left

@@ -134,3 +134,50 @@ def test_bgzf_feed_corrupt_member(tmp_path, monkeypatch):
     open(comp, "wb").write(bytes(blob))
     rk, err, _, _, _ = _consume(monkeypatch, comp, 1 << 30, 8)
     assert rk is None and err[0] is OSError
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+@pytest.mark.parametrize("chunk", [777, 65536])
+def test_bgzf_chunked_feed(tmp_path, monkeypatch, case, chunk):
+    """BGZF input through the chunk-parallel feed (each chunk inflates only the
+    members under its window): the plain file's serial result, for every
+    layout (CRLF and wrapped FASTQ fall back to the streaming feed, a
+    malformed record raises after the same reads), and the same as streaming
+    the BGZF file through one parser (KH_BGZF_CHUNKED=0)."""
+    from tests import bgzf
+    c = dict(CASES[case])
+    plain = str(tmp_path / ("in." + c.pop("kind")))
+    if plain.endswith(".fq"):
+        _write_fastq(plain, 4000, **c)
+    else:
+        _write_fasta(plain, 4000)
+    raw = open(plain, "rb").read()
+    comp = plain + ".bgz"
+    open(comp, "wb").write(bgzf.compress(raw, block=1000))
+    monkeypatch.setenv("KH_BGZF_MIN_BYTES", "1")   # the BGZF paths for a small file
+    serial = _consume(monkeypatch, plain, 1 << 30, 1)
+    assert _consume(monkeypatch, comp, chunk, 8) == serial
+    monkeypatch.setenv("KH_BGZF_CHUNKED", "0")
+    assert _consume(monkeypatch, comp, chunk, 8) == serial
+
+
+@pytest.mark.parametrize("where", ["early", "middle", "late"])
+def test_bgzf_chunked_feed_damage(tmp_path, monkeypatch, where):
+    """A damaged member under some chunk's window: the chunked feed consumes
+    exactly the reads the streaming parser returns before the damage, then
+    raises OSError (same tables, same counters)."""
+    from tests import bgzf
+    plain = str(tmp_path / "in.fq")
+    _write_fastq(plain, 4000)
+    blob = bytearray(bgzf.compress(open(plain, "rb").read(), block=1000))
+    offs = bgzf.member_offsets(bytes(blob))
+    i = {"early": 2, "middle": len(offs) // 2, "late": len(offs) - 3}[where]
+    blob[offs[i] + 30] ^= 0xFF
+    comp = str(tmp_path / "bad.fq.bgz")
+    open(comp, "wb").write(bytes(blob))
+    monkeypatch.setenv("KH_BGZF_MIN_BYTES", "1")
+    chunked = _consume(monkeypatch, comp, 4096, 8)
+    monkeypatch.setenv("KH_BGZF_CHUNKED", "0")
+    streamed = _consume(monkeypatch, comp, 4096, 8)
+    assert chunked[1] is not None and chunked[1][0] is OSError
+    assert chunked == streamed

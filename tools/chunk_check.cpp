@@ -1,0 +1,107 @@
+// Development: the chunk-parallel parse (kh_parser.cpp plain_parse_chunk /
+// plain_parse_rest, in consume_chunked's order, one thread) against the
+// streaming parser over the same file: reads parsed, a digest of the reads
+// of >= k bases, and the error.  Host only (no device).
+// Build: see tools/chunk_check.sh.  Usage: chunk_check <file> <chunk bytes> [k]
+#include <stdio.h>
+#include <stdlib.h>
+#include <functional>
+#include <string>
+#include <vector>
+#include "../khmer_amd/csrc/kh_internal.h"
+
+namespace kh {
+struct Parser;
+struct PlainFile;
+Parser *parser_open(const char *path);
+void parser_close(Parser *p);
+void parser_fill_raw(Parser *p, RawBatch &b, int k, uint64_t max_kmers, uint64_t max_bases, bool *done, uint64_t *taken);
+PlainFile *parser_plain_open(Parser *pr);
+void parser_plain_close(PlainFile *f);
+size_t plain_size(const PlainFile *f);
+bool plain_chunkable(const PlainFile *f, size_t CH);
+void plain_parse_chunk(const PlainFile *f, size_t c, size_t CH, int k, uint64_t max_kmers, std::vector<RawBatch> &out,
+                       uint64_t *nreads, size_t *start, size_t *end, bool *redo);
+void plain_parse_rest(const PlainFile *f, size_t from, size_t CH, int k, uint64_t max_kmers,
+                      const std::function<void(RawBatch &)> &sink, uint64_t *nreads);
+}  // namespace kh
+
+struct Out {
+    uint64_t reads = 0, kept = 0, h = 1469598103934665603ull;
+    std::string err;
+    void add(const kh::RawBatch &b) {
+        const char *p = b.seq.data();
+        for (uint32_t n : b.len) {
+            h = (h ^ n) * 1099511628211ull;
+            for (uint32_t i = 0; i < n; i++) h = (h ^ (unsigned char)p[i]) * 1099511628211ull;
+            p += n;
+            kept++;
+        }
+    }
+};
+
+int main(int argc, char **argv) {
+    if (argc < 3) return 2;
+    const char *path = argv[1];
+    const size_t CH = strtoull(argv[2], nullptr, 10);
+    const int k = argc > 3 ? atoi(argv[3]) : 21;
+    const uint64_t maxk = 1 << 20;
+    Out a, b;
+    try {   // streaming
+        kh::Parser *p = kh::parser_open(path);
+        for (bool done = false; !done;) {
+            kh::RawBatch r;
+            uint64_t t = 0;
+            try {
+                kh::parser_fill_raw(p, r, k, maxk, maxk * 2 + 4096, &done, &t);
+            } catch (const std::exception &e) {
+                a.reads += t;
+                a.add(r);
+                throw;
+            }
+            a.reads += t;
+            a.add(r);
+        }
+        kh::parser_close(p);
+    } catch (const std::exception &e) {
+        a.err = e.what();
+    }
+    int mode = 0;   // 0 chunked, 1 not chunkable, 2 serial rest taken
+    try {   // chunked, in consume_chunked's order
+        kh::Parser *p = kh::parser_open(path);
+        kh::PlainFile *f = kh::parser_plain_open(p);
+        if (!f) { printf("{\"chunked\": false}\n"); return 3; }
+        const size_t n = kh::plain_size(f), nch = (n + CH - 1) / CH;
+        if (nch > 1 && !kh::plain_chunkable(f, CH)) mode = 1;
+        size_t true_end = 0;
+        bool serial = mode == 1;
+        for (size_t c = 0; c < nch && !serial; c++) {
+            std::vector<kh::RawBatch> raw;
+            uint64_t nr = 0;
+            size_t s = 0, e = 0;
+            bool redo = false;
+            std::string err;
+            try {
+                kh::plain_parse_chunk(f, c, CH, k, maxk, raw, &nr, &s, &e, &redo);
+            } catch (const std::exception &x) {
+                err = x.what();
+            }
+            if (redo || (s != true_end && !(s >= n && true_end >= n))) { serial = true; mode = 2; break; }
+            for (auto &r : raw) b.add(r);
+            b.reads += nr;
+            true_end = e;
+            if (!err.empty()) throw std::runtime_error(err);
+        }
+        if (serial && true_end < n)
+            kh::plain_parse_rest(f, true_end, CH, k, maxk, [&](kh::RawBatch &r) { b.add(r); }, &b.reads);
+        kh::parser_plain_close(f);
+        kh::parser_close(p);
+    } catch (const std::exception &e) {
+        b.err = e.what();
+    }
+    const bool same = a.reads == b.reads && a.kept == b.kept && a.h == b.h && a.err == b.err;
+    printf("{\"same\": %s, \"mode\": %d, \"reads\": [%llu, %llu], \"kept\": [%llu, %llu], \"err\": [\"%s\", \"%s\"]}\n",
+           same ? "true" : "false", mode, (unsigned long long)a.reads, (unsigned long long)b.reads,
+           (unsigned long long)a.kept, (unsigned long long)b.kept, a.err.c_str(), b.err.c_str());
+    return same ? 0 : 1;
+}

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Compressed-input feed: the parity tests, then end-to-end consume_seqfile
 # rates (C2-shaped Countgraph, tools/bench_e2e.py) for plain, gzip and BGZF
-# input, serial inflate (KH_ASYNC_INFLATE=0) against the threaded one.
+# input, serial inflate (KH_ASYNC_INFLATE=0) against the threaded one, and
+# BGZF streamed through one parser (KH_BGZF_CHUNKED=0) or chunk-parallel.
 # Usage: tools/r4_gz.sh <tag> [reads]
 set -u
 tag=${1:?tag}; reads=${2:-2000000}
@@ -17,12 +18,12 @@ for c in none gzip bgzf; do
   cat "$out/make_$c.json"
 done
 run() {
-  name=$1; async=$2; f=$3
-  KH_ASYNC_INFLATE=$async timeout -k 10 400 python3 tools/bench_e2e.py --reads $reads --cpu-reads 0 --input $f > "$out/$name.json" 2> "$out/$name.err" || { echo "e2e $name failed"; tail -5 "$out/$name.err"; return 1; }
+  name=$1; async=$2; f=$3; chunked=${4:-1}
+  KH_BGZF_CHUNKED=$chunked KH_ASYNC_INFLATE=$async timeout -k 10 400 python3 tools/bench_e2e.py --reads $reads --cpu-reads 0 --input $f > "$out/$name.json" 2> "$out/$name.err" || { echo "e2e $name failed"; tail -5 "$out/$name.err"; return 1; }
   python3 -c "
 import json; d=json.loads(open('$out/$name.json').read().strip().splitlines()[-1])
 print('$name', '%.3e k-mers/s'%d['value'], '%.2f s'%d['seconds'], 'fastq %.2f GB/s'%d['fastq_GBps'], 'file %.3f GB/s'%d['file_GBps'])"
 }
 run plain 1 $d/none.fq &&
 run gzip_serial 0 $d/gzip.fq.gz && run gzip_async 1 $d/gzip.fq.gz &&
-run bgzf_serial 0 $d/bgzf.fq.bgz && run bgzf_async 1 $d/bgzf.fq.bgz
+run bgzf_serial 0 $d/bgzf.fq.bgz && run bgzf_stream 1 $d/bgzf.fq.bgz 0 && run bgzf_chunked 1 $d/bgzf.fq.bgz 1
