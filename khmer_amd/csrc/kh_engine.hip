@@ -656,7 +656,11 @@ static size_t lds_hist_l1(const Params &P, bool window) {
 // tile.  Measured on C2 (scatter_l1 ms/step): no tails 128, 2 records 108,
 // 4 records 114, 8 records 122 -- every tile flushes nearly every bucket's
 // tail, so smaller tails mean fewer LDS slot scans per tile.
-static int l1_seg(const Params &P) { return P.F1 <= 1024 ? 2 : 0; }
+static int l1_seg(const Params &P) {
+    static const int v = env_seg("KH_L1_SEG", -1);   // development A/B: 0 or 2 at any F1
+    if (v == 0 || v == 2) return v;
+    return P.F1 <= 1024 ? 2 : 0;
+}
 static size_t lds_scatter_l1(const Params &P, bool window, int tile_kmers) {
     const size_t F1a = (P.F1 + 3) & ~3u;
     const int seg = l1_seg(P);
