@@ -37,6 +37,7 @@ void parser_fill_raw(Parser *p, RawBatch &b, int k, uint64_t max_kmers, uint64_t
 struct PlainFile;
 PlainFile *parser_plain_open(Parser *pr);
 void parser_plain_close(PlainFile *f);
+void parser_plain_commit(Parser *pr);
 size_t plain_size(const PlainFile *f);
 bool plain_chunkable(const PlainFile *f, size_t CH);
 void plain_parse_chunk(const PlainFile *f, size_t c, size_t CH, int k, uint64_t max_kmers, std::vector<RawBatch> &out,
@@ -479,6 +480,7 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
     // no recognisable record start inside the second chunk (CRLF or wrapped
     // FASTQ): the streaming reader/packer pipeline instead
     if (nch > 1 && !plain_chunkable(pf, CH)) return false;
+    parser_plain_commit(parser);
     const int T = std::max(1, feed_threads() - 1);
     const size_t depth = (size_t)T * 2;
     const uint64_t maxk = std::min<uint64_t>(g->batch_kmers, 1ull << 27);

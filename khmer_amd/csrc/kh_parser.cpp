@@ -718,6 +718,12 @@ PlainFile *parser_plain_open(Parser *pr) {
     }
     return f.release();
 }
+// the chunk path takes the file: a BGZF parser's own inflate workers stop
+// (they would inflate groups nobody reads); the parser is drained afterwards
+void parser_plain_commit(Parser *pr) {
+    std::lock_guard<std::mutex> lk(pr->mu);
+    if (BgzfSource *b = dynamic_cast<BgzfSource *>(pr->src.get())) b->stop_threads();
+}
 void parser_plain_close(PlainFile *f) { delete f; }
 size_t plain_size(const PlainFile *f) { return f->n; }
 

@@ -3,9 +3,15 @@
 // streaming parser over the same file: reads parsed, a digest of the reads
 // of >= k bases, and the error.  Host only (no device).
 // Build: see tools/chunk_check.sh.  Usage: chunk_check <file> <chunk bytes> [k]
+// Timing: chunk_check <file> <chunk bytes> <k> <threads> -- the chunks parsed
+// on <threads> threads (no ordering or fallback), against the streaming
+// parser, wall-clock rates.
 #include <stdio.h>
 #include <stdlib.h>
+#include <atomic>
+#include <chrono>
 #include <functional>
+#include <thread>
 #include <string>
 #include <vector>
 #include "../khmer_amd/csrc/kh_internal.h"
@@ -17,6 +23,7 @@ Parser *parser_open(const char *path);
 void parser_close(Parser *p);
 void parser_fill_raw(Parser *p, RawBatch &b, int k, uint64_t max_kmers, uint64_t max_bases, bool *done, uint64_t *taken);
 PlainFile *parser_plain_open(Parser *pr);
+void parser_plain_commit(Parser *pr);
 void parser_plain_close(PlainFile *f);
 size_t plain_size(const PlainFile *f);
 bool plain_chunkable(const PlainFile *f, size_t CH);
@@ -40,11 +47,61 @@ struct Out {
     }
 };
 
+static double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static int timing(const char *path, size_t CH, int k, int T) {
+    const uint64_t maxk = 1 << 20;
+    double t0 = now();
+    uint64_t r0 = 0;
+    {
+        kh::Parser *p = kh::parser_open(path);
+        for (bool done = false; !done;) {
+            kh::RawBatch r;
+            kh::parser_fill_raw(p, r, k, maxk, maxk * 2 + 4096, &done, &r0);
+        }
+        kh::parser_close(p);
+    }
+    const double ts = now() - t0;
+    t0 = now();
+    kh::Parser *p = kh::parser_open(path);
+    kh::PlainFile *f = kh::parser_plain_open(p);
+    if (!f) { printf("{\"chunked\": false}\n"); return 3; }
+    kh::parser_plain_commit(p);
+    const size_t n = kh::plain_size(f), nch = (n + CH - 1) / CH;
+    std::atomic<size_t> next{0};
+    std::atomic<uint64_t> reads{0}, redo{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+        th.emplace_back([&] {
+            for (size_t c; (c = next++) < nch;) {
+                std::vector<kh::RawBatch> raw;
+                uint64_t nr = 0;
+                size_t s = 0, e = 0;
+                bool rd = false;
+                kh::plain_parse_chunk(f, c, CH, k, maxk, raw, &nr, &s, &e, &rd);
+                reads += nr;
+                redo += rd;
+            }
+        });
+    for (auto &x : th) x.join();
+    const double tc = now() - t0;
+    printf("{\"file\": \"%s\", \"stream_bytes\": %zu, \"threads\": %d, \"streaming_s\": %.3f, \"streaming_GBps\": %.3f, "
+           "\"chunked_s\": %.3f, \"chunked_GBps\": %.3f, \"reads\": [%llu, %llu], \"redo\": %llu}\n",
+           path, n, T, ts, n / ts / 1e9, tc, n / tc / 1e9, (unsigned long long)r0, (unsigned long long)reads.load(),
+           (unsigned long long)redo.load());
+    kh::parser_plain_close(f);
+    kh::parser_close(p);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 3) return 2;
     const char *path = argv[1];
     const size_t CH = strtoull(argv[2], nullptr, 10);
     const int k = argc > 3 ? atoi(argv[3]) : 21;
+    if (argc > 4) return timing(path, CH, k, atoi(argv[4]));
     const uint64_t maxk = 1 << 20;
     Out a, b;
     try {   // streaming
