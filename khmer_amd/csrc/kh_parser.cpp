@@ -815,7 +815,7 @@ static void chunk_parser(Parser &pr, const PlainFile *f, const unsigned char *p,
     ms->pos = 0;
     pr.src = std::move(ms);
     pr.path = f->path;
-    pr.buf.resize(1 << 22);
+    pr.buf.resize(std::min<size_t>(1 << 22, std::max<size_t>(nbytes, 4096)));
     pr.fastq = f->fastq;
     pr.have_qualities = f->fastq;
     pr.num_reads = 1;
