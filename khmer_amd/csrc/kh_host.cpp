@@ -1,5 +1,6 @@
 // kh_host.cpp -- host-side helpers of libkhmer_hip.so: scalar hashing
 // utilities (the khmer._khmer module functions), primes, read packing.
+#include <immintrin.h>
 #include <math.h>
 #include <string.h>
 
@@ -107,6 +108,43 @@ struct Maps {
 };
 static const Maps g_maps;
 
+// 8 cleaned bases -> 16 bits, first base in the top bits (BMI2 pext; x86-64
+// hosts with BMI2, checked once at run time).  A byte b is a valid base iff
+// (b | 0x20) is 'a', 'c', 'g' or 't' (exactly upper- and lower-case ACGT);
+// its code is ((b >> 1) & 3) with the two bits swapped (A 0, C 2, G 3, T 1),
+// anything else cleans to 'A' (0): _to_valid_dna + twobit_repr
+// (src/oxli/read_parsers.cc:53-69, include/oxli/kmer_hash.hh:62-70).
+__attribute__((target("bmi2"))) static inline uint32_t pack8_clean(uint64_t x) {
+    const uint64_t L = 0x0101010101010101ull, H7 = 0x7F7F7F7F7F7F7F7Full;
+    const uint64_t v = x | (0x20 * L);
+    auto eq = [&](uint64_t c) {   // 0x80 in the bytes of v equal to c
+        const uint64_t t = v ^ (c * L);
+        return ~(((t & H7) + H7) | t | H7);
+    };
+    const uint64_t valid = eq('a') | eq('c') | eq('g') | eq('t');
+    const uint64_t y = (x >> 1) & (3 * L);
+    uint64_t z = ((y & L) << 1) | ((y >> 1) & L);
+    z &= (valid >> 7) * 0xFF;
+    return (uint32_t)_pext_u64(__builtin_bswap64(z), 3 * L);
+}
+__attribute__((target("bmi2"))) static size_t pack_body_bmi2(const char *s, size_t len, uint64_t *dst) {
+    size_t i = 0, w = 0;
+    for (; i + 32 <= len; i += 32, w++) {
+        uint64_t q[4];
+        memcpy(q, s + i, 32);
+        dst[w] = ((uint64_t)pack8_clean(q[0]) << 48) | ((uint64_t)pack8_clean(q[1]) << 32) |
+                 ((uint64_t)pack8_clean(q[2]) << 16) | (uint64_t)pack8_clean(q[3]);
+    }
+    return i;
+}
+static bool have_bmi2() {
+    static const bool v = [] {
+        const char *e = getenv("KH_PACK_SCALAR");   // development A/B
+        return !(e && atoi(e)) && __builtin_cpu_supports("bmi2");
+    }();
+    return v;
+}
+
 void HostBatch::append(const char *s, size_t len, int k, bool clean) {
     uint64_t nk = len - (uint64_t)k + 1;
     if (hash == MURMUR) {
@@ -127,6 +165,11 @@ void HostBatch::append(const char *s, size_t len, int k, bool clean) {
             i++; p++;
         }
         // body: 32 bases per word
+        if (clean && have_bmi2() && i + 32 <= len) {
+            const size_t done = pack_body_bmi2(s + i, len - i, words.data() + (p >> 5));
+            i += done;
+            p += done;
+        }
         while (i + 32 <= len) {
             uint64_t w = 0;
             for (int b = 0; b < 32; b++) w = (w << 2) | mp[(uint8_t)s[i + b]];

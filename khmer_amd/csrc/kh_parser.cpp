@@ -41,6 +41,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -461,14 +462,43 @@ std::unique_ptr<Source> open_source(const char *path) {
 }  // namespace
 
 // isspace() of the C locale as a table (space, \t, \n, \v, \f, \r)
-static const unsigned char *ws_tab() {
-    static const struct T {
-        unsigned char t[256];
-        T() {
-            for (int c = 0; c < 256; c++) t[c] = isspace(c) ? 1 : 0;
+struct WsTab {
+    unsigned char t[256];
+    WsTab() {
+        for (int c = 0; c < 256; c++) t[c] = isspace(c) ? 1 : 0;
+    }
+};
+static const WsTab g_ws;
+
+// The first whitespace byte in [q, e) (e if none): 16 bytes a step with SSE2
+// (x86-64 baseline) -- every whitespace byte is <= 0x20, so only the bytes
+// <= 0x20 of a block are checked against the table.
+static inline const unsigned char *find_ws(const unsigned char *q, const unsigned char *e) {
+    const __m128i lim = _mm_set1_epi8(0x20);
+    while (e - q >= 16) {
+        const __m128i x = _mm_loadu_si128((const __m128i *)q);
+        unsigned m = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_max_epu8(x, lim), lim));
+        while (m) {
+            const int b = __builtin_ctz(m);
+            if (g_ws.t[q[b]]) return q + b;
+            m &= m - 1;
         }
-    } tab;
-    return tab.t;
+        q += 16;
+    }
+    while (q < e && !g_ws.t[*q]) q++;
+    return q;
+}
+// The first '\n' or '\r' in [q, e) (e if none)
+static inline const unsigned char *find_eol(const unsigned char *q, const unsigned char *e) {
+    const __m128i nl = _mm_set1_epi8('\n'), cr = _mm_set1_epi8('\r');
+    while (e - q >= 16) {
+        const __m128i x = _mm_loadu_si128((const __m128i *)q);
+        const unsigned m = (unsigned)_mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(x, nl), _mm_cmpeq_epi8(x, cr)));
+        if (m) return q + __builtin_ctz(m);
+        q += 16;
+    }
+    while (q < e && *q != '\n' && *q != '\r') q++;
+    return q;
 }
 
 struct Parser {
@@ -507,8 +537,7 @@ struct Parser {
             if (pos >= len && peek() < 0) return;
             // fast scan of the buffered chunk
             unsigned char *s = buf.data() + pos, *e = buf.data() + len;
-            unsigned char *q = s;
-            while (q < e && *q != '\n' && *q != '\r') q++;
+            unsigned char *q = (unsigned char *)find_eol(s, e);
             out.append((const char *)s, (size_t)(q - s));
             pos += (size_t)(q - s);
             if (q < e) {
@@ -542,8 +571,8 @@ struct Parser {
             if (c == '\r' || c == '\n') { after_eol = true; pos++; continue; }
             if (after_eol && c == stop) break;
             // fast path: copy a run of sequence characters
-            unsigned char *s = buf.data() + pos, *e = buf.data() + len, *q = s;
-            while (q < e && !ws_tab()[*q]) q++;
+            unsigned char *s = buf.data() + pos, *e = buf.data() + len;
+            unsigned char *q = (unsigned char *)find_ws(s, e);
             if (q == s) { pos++; after_eol = false; continue; }  // isolated space
             seq.append((const char *)s, (size_t)(q - s));
             pos += (size_t)(q - s);
@@ -564,8 +593,7 @@ struct Parser {
             unsigned char *s = buf.data() + pos, *e = buf.data() + len;
             const size_t need = seq.size() - qual.size();
             unsigned char *lim = (size_t)(e - s) > need ? s + need : e;
-            unsigned char *q = s;
-            while (q < lim && !ws_tab()[*q]) q++;
+            unsigned char *q = (unsigned char *)find_ws(s, lim);
             if (q == s) { pos++; continue; }   // a whitespace character
             qual.append((const char *)s, (size_t)(q - s));
             pos += (size_t)(q - s);

@@ -81,3 +81,15 @@ def test_chunk_parse_bgzf_damage(tmp_path, checker, where):
         r = _run(checker, bad, chunk)
         assert r["same"] and r["err"][0].startswith("File "), (chunk, r)
         assert 0 < r["reads"][0] < 4000 or where == "early"
+
+
+@pytest.mark.parametrize("scalar", ["0", "1"])
+def test_pack_matches_restatement(checker, scalar):
+    """HostBatch::append's cleaned 2-bit packing (BMI2 fast path, or the
+    table loop with KH_PACK_SCALAR=1) against a scalar restatement of
+    _to_valid_dna + twobit_repr over random reads of every byte value."""
+    import json
+    env = dict(os.environ, KH_PACK_SCALAR=scalar)
+    r = subprocess.run([checker, "--pack", "20000"], capture_output=True, text=True, env=env, timeout=120)
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["mismatches"] == 0 and d["pack_bases"] > 3_000_000

@@ -96,7 +96,35 @@ static int timing(const char *path, size_t CH, int k, int T) {
     return 0;
 }
 
+// pack check: HostBatch::append(clean) against a scalar restatement of
+// _to_valid_dna + twobit_repr on random reads over all byte values
+static int pack_check(uint64_t seed, int nreads) {
+    auto rnd = [&]() { seed ^= seed << 13; seed ^= seed >> 7; seed ^= seed << 17; return seed; };
+    const char alpha[] = "ACGTACGTACGTacgtNnXx \t\n@+";
+    kh::HostBatch b;
+    std::vector<uint8_t> codes;
+    for (int r = 0; r < nreads; r++) {
+        const size_t len = 21 + rnd() % 300;
+        std::string s(len, 'A');
+        for (auto &c : s) c = (rnd() % 8) ? alpha[rnd() % (sizeof alpha - 1)] : (char)(rnd() & 0xFF);
+        b.append(s.data(), s.size(), 21, true);
+        for (unsigned char c : s) {
+            char cc = (c == 'A' || c == 'C' || c == 'G' || c == 'T') ? (char)c
+                      : (c == 'a' || c == 'c' || c == 'g' || c == 't') ? (char)(c - 32) : 'A';
+            codes.push_back(cc == 'A' ? 0 : cc == 'T' ? 1 : cc == 'C' ? 2 : 3);
+        }
+    }
+    uint64_t bad = 0;
+    for (size_t i = 0; i < codes.size(); i++) {
+        const uint32_t got = (uint32_t)(b.words[i >> 5] >> (62 - 2 * (i & 31))) & 3;
+        bad += got != codes[i];
+    }
+    printf("{\"pack_bases\": %zu, \"mismatches\": %llu}\n", codes.size(), (unsigned long long)bad);
+    return bad ? 1 : 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc == 3 && std::string(argv[1]) == "--pack") return pack_check(0x9E3779B97F4A7C15ull, atoi(argv[2]));
     if (argc < 3) return 2;
     const char *path = argv[1];
     const size_t CH = strtoull(argv[2], nullptr, 10);
