@@ -529,6 +529,22 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
     uint64_t total = 0;
     size_t true_end = 0;   // where the reads consumed so far really end
     bool serial_rest = false;
+    // the chunks' packed batches go to the device merged up to `lim` k-mers
+    // (a device pass per ~27M-k-mer chunk batch would cost its fixed
+    // overheads 50 times per 1.3e9 k-mers)
+    const uint64_t lim = std::min<uint64_t>(g->batch_kmers, 1ull << 30);
+    HostBatch acc;
+    acc.hash = hash;
+    auto flush = [&] {
+        if (acc.nkmers()) consume_batch(g, acc, mode, consumed);
+        acc = HostBatch();
+        acc.hash = hash;
+    };
+    auto take = [&](HostBatch &b) {
+        if (acc.nkmers() && acc.nkmers() + b.nkmers() > lim) flush();
+        if (!acc.nkmers()) acc = std::move(b);
+        else acc.merge(b);
+    };
     try {
         for (size_t c = 0; c < nch; c++) {
             {
@@ -543,12 +559,13 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
                 break;
             }
             for (HostBatch &b : C.packed) {
-                consume_batch(g, b, mode, consumed);
+                take(b);
                 HostBatch().words.swap(b.words);
             }
             total += C.nreads;
             true_end = C.end;
             if (C.err) {
+                flush();
                 *nreads_out = total;
                 parser_mark_drained(parser, total);
                 std::rethrow_exception(C.err);
@@ -565,6 +582,7 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
         throw;
     }
     finish();
+    flush();
     // the rest of the input serially
     if (serial_rest && true_end < n) {
         try {

@@ -187,4 +187,32 @@ void HostBatch::append(const char *s, size_t len, int k, bool clean) {
     read_kmers.push_back((uint32_t)nk);
 }
 
+void HostBatch::merge(const HostBatch &o) {
+    if (hash == MURMUR) {
+        bytes.insert(bytes.end(), o.bytes.begin(), o.bytes.end());
+    } else if (o.nbases) {
+        // o's bases start at base nbases: its words shifted right by the
+        // offset inside the partial word (bits past nbases are zero)
+        const uint64_t p = nbases, nw = (o.nbases + 31) / 32;
+        const uint64_t need = (p + o.nbases + 31) / 32 + 1;
+        if (words.size() < need) words.resize(need, 0);
+        uint64_t *d = words.data() + (p >> 5);
+        const unsigned sh = 2 * (unsigned)(p & 31);
+        if (sh == 0) {
+            memcpy(d, o.words.data(), nw * 8);
+        } else {
+            for (uint64_t i = 0; i < nw; i++) {
+                d[i] |= o.words[i] >> sh;
+                d[i + 1] = o.words[i] << (64 - sh);
+            }
+        }
+    }
+    const uint64_t base = koff.back();
+    for (size_t i = 1; i < o.koff.size(); i++) koff.push_back(base + o.koff[i]);
+    if (!read_kmers.empty() && !o.read_kmers.empty() && read_kmers.back() != o.read_kmers.front()) uniform = false;
+    uniform = uniform && o.uniform;
+    read_kmers.insert(read_kmers.end(), o.read_kmers.begin(), o.read_kmers.end());
+    nbases += o.nbases;
+}
+
 }  // namespace kh

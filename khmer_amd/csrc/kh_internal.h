@@ -289,6 +289,8 @@ struct HostBatch {
     }
     // append a read (reads shorter than k are skipped by the caller)
     void append(const char *s, size_t len, int k, bool clean);
+    // append batch o's reads after this batch's (same hash kind)
+    void merge(const HostBatch &o);
 };
 
 // raw reads for the pipelined host feed: concatenated sequences >= k bases

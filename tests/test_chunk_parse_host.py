@@ -93,3 +93,4 @@ def test_pack_matches_restatement(checker, scalar):
     r = subprocess.run([checker, "--pack", "20000"], capture_output=True, text=True, env=env, timeout=120)
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["mismatches"] == 0 and d["pack_bases"] > 3_000_000
+    assert d["merge_mismatch"] == 0   # HostBatch::merge of random batch splits == one batch

@@ -119,8 +119,26 @@ static int pack_check(uint64_t seed, int nreads) {
         const uint32_t got = (uint32_t)(b.words[i >> 5] >> (62 - 2 * (i & 31))) & 3;
         bad += got != codes[i];
     }
-    printf("{\"pack_bases\": %zu, \"mismatches\": %llu}\n", codes.size(), (unsigned long long)bad);
-    return bad ? 1 : 0;
+    // merge: batches of random sizes merged in order equal one batch
+    kh::HostBatch m, part;
+    uint64_t seed2 = seed;
+    seed = 0x9E3779B97F4A7C15ull;
+    for (int r = 0; r < nreads; r++) {
+        const size_t len = 21 + rnd() % 300;
+        std::string s(len, 'A');
+        for (auto &c : s) c = (rnd() % 8) ? alpha[rnd() % (sizeof alpha - 1)] : (char)(rnd() & 0xFF);
+        part.append(s.data(), s.size(), 21, true);
+        if ((r * 2654435761u) % 7 == 0 || r + 1 == nreads) {
+            m.merge(part);
+            part = kh::HostBatch();
+        }
+    }
+    (void)seed2;
+    uint64_t mbad = (m.nbases != b.nbases) * 1 + (m.koff != b.koff) * 2 + (m.read_kmers != b.read_kmers) * 4 + (m.uniform != b.uniform) * 8;
+    for (uint64_t i = 0; i < (b.nbases + 31) / 32 && !mbad; i++) mbad += m.words[i] != b.words[i];
+    printf("{\"pack_bases\": %zu, \"mismatches\": %llu, \"merge_mismatch\": %llu}\n", codes.size(),
+           (unsigned long long)bad, (unsigned long long)mbad);
+    return bad || mbad ? 1 : 0;
 }
 
 int main(int argc, char **argv) {
