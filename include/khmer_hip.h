@@ -77,7 +77,7 @@ int kh_get_n_primes_near_x(uint32_t n, uint64_t x, uint64_t *out, uint32_t *foun
  * replaces oxli::read_parsers::ReadParser<FastxReader> and the CPython
  * khmer.ReadParser (include/oxli/read_parsers.hh:138-178,
  * src/oxli/read_parsers.cc:257-382, src/khmer/_cpy_readparsers.cc:392-550).
- * FASTA/FASTQ, plain or gzip. */
+ * FASTA/FASTQ: plain, gzip (incl. BGZF / concatenated members) or bzip2. */
 int  kh_parser_open(const char *path, kh_parser **out);
 /* next read; returns KH_END when exhausted.  Pointers stay valid until the
  * next call on this parser from the same thread. */

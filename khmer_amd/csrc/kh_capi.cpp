@@ -528,6 +528,16 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
     };
     uint64_t total = 0;
     size_t true_end = 0;   // where the reads consumed so far really end
+    // after parser_plain_commit the parser's own source is stopped: every exit
+    // (errors included) must mark it drained exactly once, or a later read
+    // from it would wait forever for a producer that is gone
+    bool drained = false;
+    auto drain = [&] {
+        if (drained) return;
+        drained = true;
+        *nreads_out = total;
+        parser_mark_drained(parser, total);
+    };
     bool serial_rest = false;
     // the chunks' packed batches go to the device merged up to `lim` k-mers
     // (a device pass per ~27M-k-mer chunk batch would cost its fixed
@@ -566,8 +576,7 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
             true_end = C.end;
             if (C.err) {
                 flush();
-                *nreads_out = total;
-                parser_mark_drained(parser, total);
+                drain();
                 std::rethrow_exception(C.err);
             }
             {
@@ -579,10 +588,16 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
         }
     } catch (...) {
         finish();
+        drain();
         throw;
     }
     finish();
-    flush();
+    try {
+        flush();
+    } catch (...) {
+        drain();
+        throw;
+    }
     // the rest of the input serially
     if (serial_rest && true_end < n) {
         try {
@@ -592,13 +607,11 @@ static bool consume_chunked(Graph *g, Parser *parser, PlainFile *pf, int mode, u
                 consume_batch(g, b, mode, consumed);
             }, &total);
         } catch (...) {
-            *nreads_out = total;
-            parser_mark_drained(parser, total);
+            drain();
             throw;
         }
     }
-    *nreads_out = total;
-    parser_mark_drained(parser, total);
+    drain();
     return true;
 }
 
@@ -730,10 +743,18 @@ int kh_consume_parser(kh_graph *h, kh_parser *ph, int mode, uint32_t *reads, uin
                 consume_pipelined(g, ph->p, mode, &nreads, &consumed);
             } catch (...) {
                 t_tagpipe = nullptr;
-                // the reads before the error are consumed and tagged
-                if (tp) consumed += tp->finish();
+                // the reads before the error are consumed and tagged; the
+                // caller sees the original error (a tagger failure of its
+                // own would otherwise replace it and lose the counts)
                 *reads = (uint32_t)nreads;
                 *kmers = consumed;
+                if (tp) {
+                    try {
+                        consumed += tp->finish();
+                        *kmers = consumed;
+                    } catch (...) {
+                    }
+                }
                 throw;
             }
             t_tagpipe = nullptr;

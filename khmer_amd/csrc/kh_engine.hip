@@ -184,7 +184,7 @@ static void ensure_recs(Graph *g, uint64_t recs, bool level2 = true) {
         if (!level2 && pp == &w.rec2) continue;   // level-1 only (an exchange-mode view)
         // KH_REC_MALLOC_FLAGS: development knob, hipExtMallocWithFlags flags for
         // the record buffers (placement experiments); plain hipMalloc otherwise
-        static const char *fl = getenv("KH_REC_MALLOC_FLAGS");
+        static const char *fl = dev_getenv("KH_REC_MALLOC_FLAGS");
         if (fl && atoi(fl) &&
             hipExtMallocWithFlags((void **)pp, cap * 8 + 64, (unsigned)atoi(fl)) == hipSuccess)
             continue;
@@ -211,7 +211,7 @@ static size_t lds_scatter_l2f(const Params &P) { return ((size_t)1 << P.s2) * (8
 // per pass (the capacity slack is then a few percent); KH_L2_EXACT=1 forces
 // the histogram path (development).
 static bool l2f_wanted(const Graph *g, uint64_t nkmers) {
-    static const bool off = [] { const char *e = getenv("KH_L2_EXACT"); return e && atoi(e); }();
+    static const bool off = [] { const char *e = dev_getenv("KH_L2_EXACT"); return e && atoi(e); }();
     if (off || g->l2_cool > 0) return false;
     const Params &P = g->prm;
     if ((1u << P.s2) > 1024) return false;
@@ -260,7 +260,11 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
 // ---- fixed-capacity level 1 (k_scatter_l1f) ----
 // up to 1024 buckets (the per-bucket LDS state), hashed sources with <= 8
 // tables per launch; not for shards using the owned-record filter
-static int env_seg(const char *name, int dflt) {   // development knobs
+static int env_seg(const char *name, int dflt) {   // development knobs: -DKH_DEV builds only
+    const char *e = dev_getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+static int test_env_int(const char *name, int dflt) {   // read in every build: the tests set it
     const char *e = getenv(name);
     return e && *e ? atoi(e) : dflt;
 }
@@ -271,7 +275,7 @@ static int l1f_tables_per_launch();
 // Level-1 launch windows.  k_scatter_l1f keeps per-bucket state in LDS for at
 // most 1024 buckets; a geometry with more (C4 / C5: 4 x 8e9 bins = 1908
 // buckets of 2^24 bins) runs one launch per group of consecutive tables whose
-// buckets [bb0, bb0 + nb) number at most KH_L1_WIN (default 1024).  Every
+// buckets [bb0, bb0 + nb) number at most l1f_win_max() (512).  Every
 // table starts on a bucket boundary (graph_prepare_params), so a group's
 // buckets are contiguous and each launch fills its own range of the bucket
 // buffer; the launch sees them as buckets 0 .. nb - 1 through a Params copy
@@ -291,7 +295,7 @@ struct L1Win {
 // one table per launch at C4 / C5 / C5M.
 static uint32_t l1f_win_max() {
     static const int v = [] {
-        const char *e = getenv("KH_L1_WIN");   // development A/B: buckets per launch
+        const char *e = dev_getenv("KH_L1_WIN");   // development A/B: buckets per launch
         const int x = e && *e ? atoi(e) : 512;
         return std::max(1, std::min(1024, x));
     }();
@@ -324,7 +328,7 @@ static Params win_params(const Params &P, const L1Win &w) {
     return Q;
 }
 static bool l1f_ok(const Graph *g) {
-    static const bool off = [] { const char *e = getenv("KH_L1_EXACT"); return e && atoi(e); }();
+    static const bool off = [] { const char *e = dev_getenv("KH_L1_EXACT"); return e && atoi(e); }();
     return !off && !use_own_filter(g) && !l1f_windows(g->prm, l1f_tables_per_launch()).empty();
 }
 static uint32_t device_cus(const Graph *g) {
@@ -505,7 +509,7 @@ static uint64_t bkt_plan(Graph *g, uint64_t nkmers) {
 // KH_CHECK (development): record buffers pre-filled with a sentinel; after
 // each scatter the slots still holding it (holes) are counted
 static bool check_mode() {
-    static bool v = [] { const char *e = getenv("KH_CHECK"); return e && atoi(e); }();
+    static bool v = [] { const char *e = dev_getenv("KH_CHECK"); return e && atoi(e); }();
     return v;
 }
 __global__ void k_count_sentinel(const uint64_t *r, uint64_t n, unsigned long long *out) {
@@ -1223,7 +1227,7 @@ static void pass_stage_c(Graph *g, const Src &src, PassState &ps, const PassOut 
 
 // passes of at most SMALL_PASS k-mers run k_small_pass (sequential semantics,
 // no partition); KH_SMALL_PASS overrides the threshold (0 disables)
-static uint64_t small_pass_max() { return (uint64_t)std::max(0, env_seg("KH_SMALL_PASS", 2048)); }
+static uint64_t small_pass_max() { return (uint64_t)std::max(0, test_env_int("KH_SMALL_PASS", 2048)); }
 
 template <class Src>
 static void run_pass_small(Graph *g, const Src &src, uint64_t nkmers, const PassOut *out) {
@@ -3231,22 +3235,33 @@ static void group_median_bcast(ShardGroup *G, const GroupReads &R, const QueryOu
                 KH_NCCL(ncclReduce(lc.q8, lc.q8, nk, ncclUint8, ncclMin, s, G->comm, g->stream));
                 if (own(s, 0)) root_l = 0;
             } else if (G->hosted) {
+                // MIN reduce to the source only (an alltoallv whose only
+                // destination is s), in slices of at most 256 MB: the source
+                // holds W slices at a time, every other rank one (ADVICE r4:
+                // an all-gather of whole passes held W x 3.3 GB per rank)
                 Graph *g = G->shards[0];
                 auto &lc = G->loc[0];
-                std::vector<uint8_t> mine(nk), all((size_t)W * nk);
-                KH_HIP(hipMemcpyAsync(mine.data(), lc.q8, nk, hipMemcpyDeviceToHost, g->stream));
-                KH_HIP(hipStreamSynchronize(g->stream));
-                host_rc(G->tp.allgather(G->tp.ctx, mine.data(), all.data(), nk), "allgather");
-                if (own(s, 0)) {
-                    for (uint64_t q = 0; q < nk; q++) {
+                const bool root = own(s, 0);
+                const uint64_t piece = std::min<uint64_t>(nk, 256ull << 20);
+                std::vector<uint8_t> mine(piece), all(root ? (size_t)W * piece : 1);
+                std::vector<uint64_t> sb(W, 0), rb(W, 0);
+                for (uint64_t a = 0; a < nk; a += piece) {
+                    const uint64_t n = std::min(piece, nk - a);
+                    KH_HIP(hipMemcpyAsync(mine.data(), lc.q8 + a, n, hipMemcpyDeviceToHost, g->stream));
+                    KH_HIP(hipStreamSynchronize(g->stream));
+                    sb[s] = n;
+                    for (int t = 0; t < W; t++) rb[t] = root ? n : 0;
+                    host_rc(G->tp.alltoallv(G->tp.ctx, mine.data(), sb.data(), all.data(), rb.data()), "alltoallv");
+                    if (!root) continue;
+                    for (uint64_t q = 0; q < n; q++) {
                         uint8_t c = 0xFF;
-                        for (int t = 0; t < W; t++) c = std::min(c, all[(size_t)t * nk + q]);
+                        for (int t = 0; t < W; t++) c = std::min(c, all[(size_t)t * n + q]);
                         mine[q] = c;
                     }
-                    KH_HIP(hipMemcpyAsync(lc.q8, mine.data(), nk, hipMemcpyHostToDevice, g->stream));
+                    KH_HIP(hipMemcpyAsync(lc.q8 + a, mine.data(), n, hipMemcpyHostToDevice, g->stream));
                     KH_HIP(hipStreamSynchronize(g->stream));
-                    root_l = 0;
                 }
+                if (root) root_l = 0;
             } else {
                 for (int l = 0; l < NL; l++) KH_HIP(hipStreamSynchronize(G->shards[l]->stream));
                 Graph *g = G->shards[s];

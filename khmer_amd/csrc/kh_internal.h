@@ -68,6 +68,21 @@ struct Geometry {
     uint32_t bucket_table[8192];
 };
 
+// Development knobs: the environment variables that switch kernel paths or
+// schedules for A/B timing (INTEGRATION.md "Development knobs") are read only
+// by a development build (make DEV=1, i.e. -DKH_DEV); the product library
+// ignores them and always takes its defaults.  Variables the test suite sets
+// (feed chunk sizes, the owned-filter thresholds, KH_SMALL_PASS, the BGZF and
+// packer switches) are read with getenv in every build.
+static inline const char *dev_getenv(const char *name) {
+#ifdef KH_DEV
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
 // kernel parameter block (passed by value)
 // Timing-only ablations (bench.py --ablate, tools/lb_ablate.sh): switches that
 // skip work and give wrong tables.  They exist only in a development build

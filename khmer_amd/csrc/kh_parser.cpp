@@ -287,7 +287,11 @@ size_t bgzf_inflate(z_stream &z, const unsigned char *p, const BgzfMember &m, un
     inflateReset(&z);
     z.next_in = (Bytef *)(p + m.cdata);
     z.avail_in = m.clen;
-    z.next_out = dst;
+    // an empty member (ISIZE 0, e.g. the 28-byte EOF marker alone in a member
+    // group) may come with no output buffer at all: zlib refuses a null
+    // next_out (Z_STREAM_ERROR) even when there is nothing to write
+    unsigned char none = 0;
+    z.next_out = dst ? dst : &none;
     z.avail_out = m.isize;
     const int rc = inflate(&z, Z_FINISH);
     const size_t got = m.isize - z.avail_out;
@@ -422,7 +426,7 @@ struct ReadAheadSource : RingSource {
 };
 
 static bool async_off() {
-    static const bool v = [] { const char *e = getenv("KH_ASYNC_INFLATE"); return e && atoi(e) == 0; }();
+    static const bool v = [] { const char *e = dev_getenv("KH_ASYNC_INFLATE"); return e && atoi(e) == 0; }();
     return v;
 }
 

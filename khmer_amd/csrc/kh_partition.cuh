@@ -524,7 +524,10 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
     uint64_t j0 = min(nkmers, (uint64_t)blockIdx.x * CK);     // this tile's first k-mer
     uint64_t ce = min(nkmers, j0 + CK);                       // the chunk's end
     bool chunk_top = true;                                    // first tile of a chunk: take one from the queue
-    uint32_t *s_q = s_wtot + 15;                              // [1] chunk taken from the queue (the scan uses 8 slots)
+    uint32_t *s_q = s_wtot + 15;                              // [1] chunk taken from the queue
+    // the run-start scan writes one wave total per wave into s_wtot[0, waves):
+    // it must never reach the queue slot (a 1024-thread build once did and hung)
+    static_assert(L1_THREADS / 64 < 15, "k_scatter_l1f: the scan's wave totals would overwrite s_q");
     const bool pre = !needs_window(src);
     constexpr int NPEND = TW ? 1 : KPT;
     typename Src::Pend pend[NPEND];
@@ -1008,7 +1011,9 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
     uint64_t j0 = min(nkmers, (uint64_t)blockIdx.x * CK);
     uint64_t ce = min(nkmers, j0 + CK);
     bool chunk_top = true;
-    uint32_t *s_q = s_wtot + 47;   // the batch scan uses s_wtot[32, 40)
+    uint32_t *s_q = s_wtot + 47;   // the batch scan uses s_wtot[32, 32 + waves)
+    static_assert(L1_THREADS / 64 <= 15, "k_own_l1f: the batch scan's wave totals would overwrite s_q");
+    static_assert(L1_THREADS / 64 <= 16, "k_own_l1f: the tile scans use 16 wave-total slots per parity");
     constexpr int NPEND = TW ? 1 : KPT;
     typename Src::Pend pend[NPEND];
     if (!TW) {

@@ -42,7 +42,19 @@ CONFIGS = {
                        genome=50_000_000, batch_kmers=1 << 27),
     "c5m_genomic": dict(kind=7, hash=1, k=51, n=4, x=8e9, reads=1_000_000, L=150, bigcount=False,
                         genome=10_000_000, batch_kmers=1 << 26),
+    # BASELINE C4 (`bench.py --config C4`, 50M reads: one GPU, or strong-scaled
+    # over G ranks): 4 x 8e9 bytes; 32 GB of host memory for the oracle
+    "c4_50m": dict(kind=1, hash=0, k=21, n=4, x=8e9, reads=50_000_000, L=150, bigcount=True,
+                   genome=0, batch_kmers=3200 << 20),
 }
+
+# Weak-scaling streams of `bench.py --gpus G` (C2, 50M reads per rank: rank r
+# consumes reads [r * 50M, (r + 1) * 50M)): the whole job is reads [0, G * 50M).
+# The rank-order fixtures are prefixes of one stream and are made in one oracle
+# pass with snapshots (make_full_fixtures.py --snapshots).
+WEAK = {"c2_w2": 2, "c2_w4": 4, "c2_w8": 8}
+for _name, _g in WEAK.items():
+    CONFIGS[_name] = dict(CONFIGS["c2_full"], reads=50_000_000 * _g, batch_kmers=3200 << 20)
 
 # Exchange-mode (Option A) streams: a `world`-rank group consumes reads
 # [s * reads / world, (s + 1) * reads / world) on rank s in passes that take
@@ -60,6 +72,11 @@ EXCHANGE = {
     "c5m_shape_x8": ("c5m_shape", 8, 1 << 26),
     "c5m_genomic_x2": ("c5m_genomic", 2, 1 << 26),
     "c5m_genomic_x8": ("c5m_genomic", 8, 1 << 26),
+    # bench.py --gpus G (weak scaling, exchange mode, default batch): exact
+    # n_unique / bigcounts for the driver's scaling lines
+    "c2_w2_x": ("c2_w2", 2, 3200 << 20),
+    "c2_w4_x": ("c2_w4", 4, 3200 << 20),
+    "c2_w8_x": ("c2_w8", 8, 3200 << 20),
 }
 for _name, (_base, _world, _batch) in EXCHANGE.items():
     CONFIGS[_name] = dict(CONFIGS[_base], exchange=[_world, _batch])

@@ -5,6 +5,11 @@ single-threaded semantics).  Each fixture holds the per-table SHA-256, the
 counters and the bigcount-map digest of one tests/full_digest.CONFIGS entry.
 
     python tests/golden/make_full_fixtures.py c2_full c3_shape ...
+    python tests/golden/make_full_fixtures.py --snapshots c2_w2 c2_w4 c2_w8
+
+--snapshots: configurations that differ only in their read count and are
+consumed in stream order (no exchange interleave) are prefixes of one stream;
+one oracle pass writes each fixture when the stream reaches its read count.
 
 Runs on the CPU (the c2_full run hashes 6.5e9 k-mers: ~7 min, 4 GB of tables;
 c4_shape needs 32 GB of host memory)."""
@@ -21,23 +26,21 @@ from khmer_amd import synth  # noqa: E402
 from tests import full_digest as FD  # noqa: E402
 
 
-def make(name):
-    c = FD.CONFIGS[name]
+def _table(c):
     sizes = O.get_n_primes_near_x(c["n"], c["x"])
     t = O.Table(c["kind"], c["k"], sizes, hash=c["hash"])
     t.set_use_bigcount(c["bigcount"])
-    t0 = time.time()
-    kmers = 0
-    for r0, nr in FD.stream_chunks(c):
-        kmers += t.consume_synth(synth.SEED, r0, nr, c["L"], genome=c["genome"])
-    secs = time.time() - t0
+    return t, sizes
+
+
+def _write(name, c, t, sizes, kmers, secs, note=""):
     nbc, bcd = FD.bigcount_digest(t.bigcounts())
     out = {
         "config": name, "params": c, "seed": synth.SEED, "table_sizes": sizes,
         "n_consumed": kmers, "n_unique_kmers": t.n_unique_kmers(), "n_occupied": t.n_occupied(),
         "table_sha256": [FD.sha256_view(t.table_view(i)) for i in range(c["n"])],
         "n_bigcounts": nbc, "bigcount_sha256": bcd,
-        "generator": "tests/golden/make_full_fixtures.py (oracle, 1 thread, %.0f s)" % secs,
+        "generator": "tests/golden/make_full_fixtures.py (oracle, 1 thread, %.0f s%s)" % (secs, note),
     }
     nmed = FD.MEDIAN_READS.get(name)
     if nmed:
@@ -57,6 +60,42 @@ def make(name):
           "%.0f s" % secs, flush=True)
 
 
+def make(name):
+    c = FD.CONFIGS[name]
+    t, sizes = _table(c)
+    t0 = time.time()
+    kmers = 0
+    for r0, nr in FD.stream_chunks(c):
+        kmers += t.consume_synth(synth.SEED, r0, nr, c["L"], genome=c["genome"])
+    _write(name, c, t, sizes, kmers, time.time() - t0)
+
+
+def make_snapshots(names):
+    """One stream-order pass over the longest configuration's reads, writing
+    every named fixture when the stream reaches its read count."""
+    cs = [FD.CONFIGS[n] for n in names]
+    base = {k: v for k, v in cs[0].items() if k != "reads"}
+    for n, c in zip(names, cs):
+        if "exchange" in c or {k: v for k, v in c.items() if k != "reads"} != base:
+            raise SystemExit("--snapshots: %s is not a read-count prefix of %s" % (n, names[0]))
+    marks = sorted((c["reads"], n) for n, c in zip(names, cs))
+    last = marks[-1][0]
+    t, sizes = _table(cs[0])
+    t0 = time.time()
+    kmers, r0, step = 0, 0, 1_000_000
+    while marks:
+        nr = min(step, marks[0][0] - r0)
+        kmers += t.consume_synth(synth.SEED, r0, nr, base["L"], genome=base["genome"])
+        r0 += nr
+        while marks and marks[0][0] == r0:
+            _, n = marks.pop(0)
+            _write(n, FD.CONFIGS[n], t, sizes, kmers, time.time() - t0,
+                   ", snapshot at read %d of a %d-read pass" % (r0, last))
+
+
 if __name__ == "__main__":
-    for name in sys.argv[1:] or sorted(FD.CONFIGS):
-        make(name)
+    if sys.argv[1:2] == ["--snapshots"]:
+        make_snapshots(sys.argv[2:])
+    else:
+        for name in sys.argv[1:] or sorted(FD.CONFIGS):
+            make(name)

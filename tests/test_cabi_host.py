@@ -262,6 +262,20 @@ def test_parser_bgzf_small_members(tmp_path):
     assert _records(str(f)) == list(O.read_fastx(plain))
 
 
+def test_parser_bgzf_eof_member_alone(tmp_path):
+    """64q + 1 members: the 28-byte empty EOF member is alone in the last
+    member group, whose ring slot has never held data (zlib refused
+    the null output buffer and the parser raised OSError after the last
+    record).  Default BGZF threshold, so the worker-thread inflate runs."""
+    from tests import bgzf
+    raw, plain = _plain_25k(tmp_path)
+    blob = bgzf.compress(raw, block=len(raw) // 128 + 1)
+    assert len(bgzf.member_offsets(blob)) % 64 == 1 and len(blob) > (1 << 20)
+    f = tmp_path / "eof_alone.fq.gz"
+    f.write_bytes(blob)
+    assert _records(str(f)) == list(O.read_fastx(plain))
+
+
 @pytest.mark.parametrize("where", ["member", "crc"])
 def test_parser_bgzf_corrupt(tmp_path, where):
     """Damage in a middle member: OSError, after exactly the records that lie
