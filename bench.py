@@ -82,10 +82,13 @@ def parse():
                          "0 = iid uniform reads")
     ap.add_argument("--strong", action="store_true",
                     help="multi-GPU strong scaling: --reads is the whole job, split over the ranks")
-    ap.add_argument("--group-mode", choices=["exchange", "broadcast"], default="exchange",
-                    help="multi-GPU: 'exchange' (Option A, default: every rank hashes only its own reads and sends "
-                         "each level-1 bucket to its owner) or 'broadcast' (Option B: reads broadcast, every rank "
-                         "hashes every k-mer and keeps its own bins' updates); DESIGN.md §6")
+    ap.add_argument("--group-mode", choices=["delta", "exchange", "broadcast"], default="delta",
+                    help="multi-GPU: 'delta' (default: every rank counts its own reads into full-size delta tables, "
+                         "owners turn every rank's deltas of their slice into per-rank prefixes, each rank applies "
+                         "its reads over its prefix; only table bytes travel), 'exchange' (Option A: every rank "
+                         "hashes only its own reads and sends each level-1 bucket to its owner) or 'broadcast' "
+                         "(Option B: reads broadcast, every rank hashes every k-mer and keeps its own bins' "
+                         "updates); DESIGN.md §6")
     ap.add_argument("--query", action="store_true",
                     help="time get_median_count over the reads (tables built from them first, untimed)")
     ap.add_argument("--ablate", type=int, default=0,
@@ -112,17 +115,17 @@ def parse():
 FIXTURE_GRAPH = {(1, 0): "Countgraph", (2, 0): "Nodegraph", (7, 0): "SmallCountgraph", (7, 1): "SmallCounttable"}
 
 
-def matching_fixture(args, total_reads, exchange=None):
+def matching_fixture(args, total_reads, order=None):
     """The oracle golden fixture (tests/golden/full/*.json, made by
     tests/golden/make_full_fixtures.py) whose workload is exactly this run's
     whole stream, if any: then the bench line carries a parity check of its
     own (counters and per-table SHA-256 against the single-threaded oracle).
-    exchange = [world, batch_kmers] for an exchange-mode group, whose stream
-    is pass-interleaved: a fixture made in that order matches exactly; failing
-    that, the rank-order fixture of the same reads (order-free outputs only).
-    Returns (fixture, exact_order)."""
+    order = (mode, [world, batch_kmers]) for an exchange- or delta-mode group,
+    whose stream is pass-interleaved: a fixture made in that order matches
+    exactly; failing that, the rank-order fixture of the same reads
+    (order-free outputs only).  Returns (fixture, exact_order)."""
     import glob
-    same_reads, interleaved = None, None
+    same_reads, interleaved, other_order = None, None, None
     for path in sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "full", "*.json"))):
         try:
             with open(path) as fh:
@@ -133,16 +136,20 @@ def matching_fixture(args, total_reads, exchange=None):
         if (FIXTURE_GRAPH.get((p["kind"], p["hash"])) == args.graph and p["k"] == args.k and p["n"] == args.tables
                 and float(p["x"]) == float(args.x) and p["reads"] == total_reads and p["L"] == args.read_len
                 and bool(p["bigcount"]) == bool(args.bigcount) and int(p["genome"]) == int(args.genome)):
-            order = p.get("exchange")
-            if order is None and same_reads is None:
+            fmode = "exchange" if "exchange" in p else "delta" if "delta" in p else None
+            if fmode is None and same_reads is None:
                 same_reads = fx
-            elif exchange is not None and order == list(exchange):
+            elif order is not None and fmode == order[0] and p[fmode] == list(order[1]):
                 interleaved = fx
-    if exchange is None:
-        return (same_reads, True) if same_reads is not None else (None, False)
-    if interleaved is not None:
+            elif fmode is not None and other_order is None:
+                other_order = fx
+    if order is None and same_reads is not None:
+        return same_reads, True
+    if order is not None and interleaved is not None:
         return interleaved, True
-    return (same_reads, False) if same_reads is not None else (None, False)
+    # the same reads in another order: the tables and n_occupied still match
+    fallback = same_reads if same_reads is not None else other_order
+    return (fallback, False) if fallback is not None else (None, False)
 
 
 def compare_fixture(fx, n_unique, n_occupied, table_sha, stream_order=True):
@@ -400,7 +407,8 @@ def main():
     check_info = runner.check()
     # parity of the timed workload itself, when a golden fixture holds it
     fx, exact_order = matching_fixture(args, nreads * world,
-                                       [world, args.batch_kmers] if (args.exchange and world > 1) else None)
+                                       (args.group_mode, [world, args.batch_kmers])
+                                       if (args.group_mode != "broadcast" and world > 1) else None)
     if args.query:
         # the tables were built untimed from the same reads; the fixture's
         # get_median_count digest (median, average, stddev of its first
@@ -484,7 +492,8 @@ def main():
                 "k": k, "n_tables": nt, "table_sizes": sizes, "reads_per_gpu": nreads,
                 "read_len": L, "kmers_per_gpu_per_step": nkmers, "bigcount": args.bigcount,
                 "batch_kmers": args.batch_kmers,
-                "parallelism": (("exchange%d" if args.exchange else "shard%d") % world) if world > 1 else "single",
+                "parallelism": ("%s%d" % ({"delta": "delta", "exchange": "exchange", "broadcast": "shard"}[args.group_mode],
+                                          world)) if world > 1 else "single",
                 "path": "get_median_count" if args.query else "consume",
                 "hash": "murmur3" if args.murmur else "twobit",
                 "genome": args.genome or None,

@@ -298,7 +298,23 @@ int kh_group_consume_packed_fixed_device(kh_group *grp, const uint64_t *const *d
  * holds the p-th chunk of every rank's reads in rank order, and n_unique /
  * bigcounts are exact for that order (tables and n_occupied do not depend on
  * the order). */
-enum { KH_GROUP_BROADCAST = 0, KH_GROUP_EXCHANGE = 1 };
+/* KH_GROUP_DELTA: the exchange-mode ownership, but no per-k-mer records
+ * travel.  Every rank partitions and counts its own chunk of a pass into
+ * full-size "delta" tables (the tables that chunk alone would give from
+ * empty tables); each owner receives every rank's delta of its slice
+ * (all-to-all), turns them into per-rank prefixes (the owned bytes as the
+ * stream saw them when that rank's chunk began: table before the pass plus
+ * the deltas of the lower ranks, saturating) and its updated slice, and
+ * sends the prefixes back (all-to-all); every rank then applies its chunk
+ * over its prefix tables with the single-GPU pipeline, which gives the
+ * exact is_new winners, occupancy and bigcount events of its own k-mers.
+ * Wire bytes per pass: 2 x the table bytes x (world - 1) / world per rank,
+ * against exchange mode's 8 bytes per (k-mer, table).  A pass takes up to
+ * the graph's batch of every rank's reads, in rank order (passes of
+ * khmer_amd.parallel.delta_passes); n_unique and bigcounts are exact for
+ * that order (src/oxli/hashtable.cc:192-228 is the reference's own
+ * partitioned consume). */
+enum { KH_GROUP_BROADCAST = 0, KH_GROUP_EXCHANGE = 1, KH_GROUP_DELTA = 2 };
 int kh_group_create_mode(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables, int world, int rank,
                          int nlocal, const int *devices, const unsigned char *uid, int mode, kh_group **out);
 int kh_group_create_hosted_mode(int storage, int hash_kind, int k, const uint64_t *sizes, int n_tables, int world,

@@ -14,7 +14,8 @@ LIB_PATH = os.environ.get("KHMER_AMD_LIB") or os.path.join(_HERE, "libkhmer_hip.
 KH_OK, KH_EVALUE, KH_EFILE, KH_EATTR, KH_ENOMEM, KH_EDEVICE, KH_ERUNTIME, KH_END = range(8)
 STORAGE_BYTE, STORAGE_BIT, STORAGE_NIBBLE = 1, 2, 7
 HASH_TWOBIT, HASH_MURMUR = 0, 1
-GROUP_BROADCAST, GROUP_EXCHANGE = 0, 1   # include/khmer_hip.h KH_GROUP_*
+GROUP_BROADCAST, GROUP_EXCHANGE, GROUP_DELTA = 0, 1, 2   # include/khmer_hip.h KH_GROUP_*
+GROUP_MODES = {"broadcast": GROUP_BROADCAST, "exchange": GROUP_EXCHANGE, "delta": GROUP_DELTA}
 
 if not os.path.exists(LIB_PATH):
     raise ImportError("khmer_amd: %s is not built; run `make -C khmer_amd/csrc` "

@@ -1243,4 +1243,152 @@ __global__ void k_full_scatter(const uint64_t *list, uint64_t n, uint8_t *fullf)
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Delta mode (group mode KH_GROUP_DELTA, kh_engine.hip group_consume_delta).
+// Every rank partitions its own chunk in the unsharded geometry, and
+// k_apply_delta writes the table that chunk ALONE would produce from empty
+// tables -- min(cap, inserts) per bin, in the storage's own layout (Byte: 1
+// B per bin; Nibble: even bin -> high nibble, storage.hh:262-272; Bit: bin b
+// -> bit b % 8 of byte b / 8, storage.hh:172-199) -- into the view's table
+// arena.  No k-mer index is needed: the table value of a bin is order-free
+// (SURVEY F4).  One workgroup of TH threads per region of R = 16 * TH bins
+// (every region is written, empty ones as zeros, so the arena needs no
+// clearing).
+template <int KIND, int TH>
+__global__ void __launch_bounds__(TH) k_apply_delta(Params P, ApplyArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int BPT = 16;
+    const uint32_t R = 1u << P.s0;
+    uint32_t *cnt = (uint32_t *)smem;   // [R]
+    const uint32_t t = threadIdx.x;
+    const uint32_t cap = KIND == BYTE ? 255u : KIND == NIBBLE ? 15u : 1u;
+    const uint64_t total = A.rprefix[P.n];
+    for (uint64_t rr = blockIdx.x; rr < total; rr += gridDim.x) {
+        const RegionInfo ri = region_info(P, A, rr, load_bounds(P, A, rr, total));
+        const bool any = ri.e0 != ri.e1;
+        if (any) {
+            for (uint32_t x = t; x < R / 4; x += TH) ((uint4 *)cnt)[x] = make_uint4(0, 0, 0, 0);
+            block_sync();
+            // 16-B record pairs, APPLY_RECS records per thread in flight
+            const uint64_t step = (uint64_t)(APPLY_RECS / 2) * TH;
+            for (uint64_t q0 = ri.e0 >> 1; 2 * q0 < ri.e1; q0 += step) {
+                uint64_t v[APPLY_RECS];
+                load_recs<TH>(A.rec, q0, ri.e0, ri.e1, v);
+#pragma unroll
+                for (int u = 0; u < APPLY_RECS; u++)
+                    if (v[u] != ~0ull) atomicAdd(&cnt[(uint32_t)v[u]], 1u);
+            }
+            block_sync();
+        }
+        // this thread's 16 bins -> their bytes of the region
+        const uint32_t b0 = BPT * t;
+        if (b0 < ri.nb) {
+            uint32_t c[BPT];
+            if (any) {
+#pragma unroll
+                for (int q = 0; q < BPT / 4; q++) {
+                    const uint4 n4 = ((const uint4 *)cnt)[4 * t + q];
+                    c[4 * q] = min(n4.x, cap);
+                    c[4 * q + 1] = min(n4.y, cap);
+                    c[4 * q + 2] = min(n4.z, cap);
+                    c[4 * q + 3] = min(n4.w, cap);
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < BPT; q++) c[q] = 0;
+            }
+            // the chunk's bytes (16 / 8 / 2) in o; a chunk that runs past the
+            // table's last byte (the arena pads tables to 256 B, and the
+            // padding may be shorter than a chunk) is written byte by byte
+            uint8_t *tab = A.tab + P.tbyte[ri.i];
+            uint32_t o[4] = {0, 0, 0, 0};
+            uint64_t at;
+            int nby;
+            if (KIND == BYTE) {
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    o[q] = c[4 * q] | c[4 * q + 1] << 8 | c[4 * q + 2] << 16 | c[4 * q + 3] << 24;
+                at = ri.bin_lo + b0;
+                nby = 16;
+            } else if (KIND == NIBBLE) {
+#pragma unroll
+                for (int q = 0; q < 2; q++)
+                    o[q] = (c[8 * q] << 4 | c[8 * q + 1]) | (c[8 * q + 2] << 4 | c[8 * q + 3]) << 8 |
+                           (c[8 * q + 4] << 4 | c[8 * q + 5]) << 16 | (c[8 * q + 6] << 4 | c[8 * q + 7]) << 24;
+                at = (ri.bin_lo + b0) >> 1;
+                nby = 8;
+            } else {
+#pragma unroll
+                for (int q = 0; q < BPT; q++) o[0] |= c[q] << q;
+                at = (ri.bin_lo + b0) >> 3;
+                nby = 2;
+            }
+            if (at + nby <= P.tbytes[ri.i]) {
+                if (KIND == BYTE) *(uint4 *)(tab + at) = make_uint4(o[0], o[1], o[2], o[3]);
+                else if (KIND == NIBBLE) *(uint2 *)(tab + at) = make_uint2(o[0], o[1]);
+                else *(uint16_t *)(tab + at) = (uint16_t)o[0];
+            } else {
+                for (int q = 0; q < nby && at + q < P.tbytes[ri.i]; q++) tab[at + q] = (uint8_t)(o[q >> 2] >> (8 * (q & 3)));
+            }
+        }
+        if (any) block_sync();   // cnt is reused by the next region
+    }
+}
+
+// The owner's prefix over ranks (delta mode): for every byte x of its slice,
+// the table value before the pass t = T[x]; rank r's chunk sees
+// P_r = t + D_0 + ... + D_{r-1} (saturating, in the storage's layout) and
+// T[x] becomes t + D_0 + ... + D_{W-1}.  buf[r * stride + x] holds D_r on
+// entry and P_r on exit.  Exact because min(cap, a + min(cap, b)) =
+// min(cap, a + b) (storage.hh:320-359, 571-624 saturate; bits OR).
+template <int KIND>
+__device__ __forceinline__ uint32_t sat_add4(uint32_t a, uint32_t b) {
+    if (KIND == BIT) return a | b;
+    uint32_t o = 0;
+    if (KIND == BYTE) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t s = ((a >> (8 * k)) & 0xFF) + ((b >> (8 * k)) & 0xFF);
+            o |= min(s, 255u) << (8 * k);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t s = ((a >> (4 * k)) & 0xF) + ((b >> (4 * k)) & 0xF);
+            o |= min(s, 15u) << (4 * k);
+        }
+    }
+    return o;
+}
+template <int KIND>
+__global__ void k_delta_prefix(uint8_t *T, uint8_t *buf, uint64_t nbytes, uint64_t stride, int W) {
+    const uint64_t n16 = nbytes / 16;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (nbytes + 15) / 16;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (i < n16) {
+            uint4 tv = ((const uint4 *)T)[i];
+            for (int r = 0; r < W; r++) {
+                uint4 *p = (uint4 *)(buf + (uint64_t)r * stride) + i;
+                const uint4 d = *p;
+                *p = tv;
+                tv = make_uint4(sat_add4<KIND>(tv.x, d.x), sat_add4<KIND>(tv.y, d.y), sat_add4<KIND>(tv.z, d.z),
+                                sat_add4<KIND>(tv.w, d.w));
+            }
+            ((uint4 *)T)[i] = tv;
+        } else {   // the slice's last < 16 bytes
+            for (uint64_t x = 16 * i; x < nbytes; x++) {
+                uint32_t tv = T[x];
+                for (int r = 0; r < W; r++) {
+                    uint8_t *p = buf + (uint64_t)r * stride + x;
+                    const uint32_t d = *p;
+                    *p = (uint8_t)tv;
+                    tv = sat_add4<KIND>(tv, d) & 0xFF;
+                }
+                T[x] = (uint8_t)tv;
+            }
+        }
+    }
+}
+
 }  // namespace kh

@@ -1537,9 +1537,9 @@ extern "C" int kh_group_create_mode(int storage, int hash_kind, int k, const uin
         CHECK_PTR(devices);
         CHECK_PTR(out);
         *out = nullptr;
-        if (mode != KH_GROUP_BROADCAST && mode != KH_GROUP_EXCHANGE) fail(KH_EVALUE, "unknown group mode");
-        ShardGroup *G = group_create(storage, hash_kind, k, sizes, n_tables, world, rank, nlocal, devices, uid,
-                                     mode == KH_GROUP_EXCHANGE);
+        if (mode != KH_GROUP_BROADCAST && mode != KH_GROUP_EXCHANGE && mode != KH_GROUP_DELTA)
+            fail(KH_EVALUE, "unknown group mode");
+        ShardGroup *G = group_create(storage, hash_kind, k, sizes, n_tables, world, rank, nlocal, devices, uid, mode);
         *out = new kh_group{G};
     });
 }
@@ -1558,9 +1558,10 @@ extern "C" int kh_group_create_hosted_mode(int storage, int hash_kind, int k, co
         CHECK_PTR(transport);
         CHECK_PTR(out);
         *out = nullptr;
-        if (mode != KH_GROUP_BROADCAST && mode != KH_GROUP_EXCHANGE) fail(KH_EVALUE, "unknown group mode");
+        if (mode != KH_GROUP_BROADCAST && mode != KH_GROUP_EXCHANGE && mode != KH_GROUP_DELTA)
+            fail(KH_EVALUE, "unknown group mode");
         ShardGroup *G = group_create_hosted(storage, hash_kind, k, sizes, n_tables, world, rank, device, transport,
-                                            mode == KH_GROUP_EXCHANGE);
+                                            mode);
         *out = new kh_group{G};
     });
 }
@@ -1627,7 +1628,7 @@ extern "C" int kh_group_mode(kh_group *grp, int *mode) {
     return guard([&] {
         CHECK_PTR(grp);
         CHECK_PTR(mode);
-        *mode = group_exchange(grp->G) ? KH_GROUP_EXCHANGE : KH_GROUP_BROADCAST;
+        *mode = group_exchange(grp->G);
     });
 }
 

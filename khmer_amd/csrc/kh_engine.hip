@@ -975,7 +975,7 @@ static void pass_apply(Graph *g, PassState &ps, bool l2f) {
 }
 
 template <class Src>
-static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
+static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool apply = true, bool *fast_out = nullptr) {
     if (nkmers > MAX_PASS_KMERS) fail(KH_EVALUE, "device batch too large (more than 3200 * 2^20 k-mers)");
     if constexpr (std::is_same<Src, SrcBytes>::value || std::is_same<Src, SrcTwoBit>::value) {
         // Murmur (the costly hash) over more than one level-1 window (or the
@@ -999,7 +999,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
             hs.kpr = 0;
             hs.kbase = 0;
             hs.h = w.frec;
-            return pass_stage_a(g, hs, nkmers);
+            return pass_stage_a(g, hs, nkmers, apply, fast_out);
         }
     }
     const Params &P = g->prm;
@@ -1154,7 +1154,8 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers) {
         }
         break;
     }
-    pass_apply(g, ps, fast);
+    if (fast_out) *fast_out = fast;
+    if (apply) pass_apply(g, ps, fast);
     return ps;
 }
 
@@ -1932,6 +1933,10 @@ struct ShardGroup {
     // and sends every bucket to its owner; rank r owns buckets [B[r], B[r+1])
     // = bins [blo, bhi) of each table ([world][n])
     bool a2a = false;
+    // delta mode (KH_GROUP_DELTA, group_consume_delta): the same ownership and
+    // views as exchange mode, but the views hold full-size tables: each rank
+    // applies its own chunk into them, and only per-bin table bytes travel
+    bool delta = false;
     std::vector<Graph *> views;
     std::vector<uint32_t> B;
     std::vector<uint64_t> blo, bhi;
@@ -1965,6 +1970,8 @@ struct ShardGroup {
         uint64_t cap_q8 = 0;         // sharded query: per-k-mer minima (owner lookups / own bins)
         uint8_t *o8 = nullptr;
         uint64_t cap_o8 = 0;         // sharded query: the reduced minima of this rank's k-mers
+        uint8_t *dbuf = nullptr;
+        uint64_t cap_dbuf = 0;       // delta mode: every rank's delta (then prefix) of the owned slices
         hipStream_t st_x = nullptr;
         hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
         bool freed[2] = {false, false};
@@ -1979,7 +1986,7 @@ struct ShardGroup {
             if (lc.st_x) (void)hipStreamSynchronize(lc.st_x);
             for (void *p : {(void *)lc.src, (void *)lc.recv, (void *)lc.ws, (void *)lc.ws_all, (void *)lc.roff,
                             (void *)lc.flist, (void *)lc.fall, (void *)lc.slot[0], (void *)lc.slot[1], (void *)lc.seg,
-                            (void *)lc.q8, (void *)lc.o8})
+                            (void *)lc.q8, (void *)lc.o8, (void *)lc.dbuf})
                 if (p) (void)hipFree(p);
             for (int b = 0; b < 2; b++) {
                 if (lc.ev_ready[b]) (void)hipEventDestroy(lc.ev_ready[b]);
@@ -2074,11 +2081,15 @@ static void a2a_plan(const Params &V, const uint64_t *sizes, int n, int world, s
 }
 
 static void group_make_shards(ShardGroup *G, int kind, int hash, int k, const uint64_t *sizes, int n,
-                              const int *devices, bool exchange) {
+                              const int *devices, int mode) {
     const int world = G->world;
+    const bool exchange = mode != 0;   // KH_GROUP_EXCHANGE or KH_GROUP_DELTA
+    G->delta = mode == 2;
     if (exchange) {
+        // exchange-mode views hold only a geometry and a workspace; delta-mode
+        // views also a full-size table arena (the rank's delta, then its prefix)
         for (int l = 0; l < G->nlocal; l++)
-            G->views.push_back(graph_build(kind, hash, k, sizes, n, devices[l], 1, 0, nullptr, nullptr, -1, false));
+            G->views.push_back(graph_build(kind, hash, k, sizes, n, devices[l], 1, 0, nullptr, nullptr, -1, G->delta));
         const Params &V = G->views[0]->prm;
         if (V.F1 < (uint32_t)world) fail(KH_EVALUE, "exchange mode needs at least one level-1 bucket per rank");
         // level 1 of the unsharded view runs in launch windows of <= 1024
@@ -2098,7 +2109,7 @@ static void group_make_shards(ShardGroup *G, int kind, int hash, int k, const ui
 }
 
 ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank, int nlocal,
-                         const int *devices, const unsigned char *uid, int exchange) {
+                         const int *devices, const unsigned char *uid, int mode) {
     if (world < 1 || world > 64) fail(KH_EVALUE, "group size must be in [1, 64]");
     if (nlocal != 1 && nlocal != world) fail(KH_EVALUE, "a process holds one shard (RCCL) or all shards (loopback)");
     if (nlocal == 1 && (rank < 0 || rank >= world)) fail(KH_EVALUE, "invalid rank");
@@ -2106,7 +2117,7 @@ ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n
     G->world = world;
     G->nlocal = nlocal;
     G->rank0 = nlocal == world ? 0 : rank;
-    group_make_shards(G.get(), kind, hash, k, sizes, n, devices, exchange != 0);
+    group_make_shards(G.get(), kind, hash, k, sizes, n, devices, mode);
     G->loc.resize(nlocal);
     // RCCL for one shard per process; a 1-rank group given a unique id runs
     // every RCCL call site too (communicator creation, split, collectives)
@@ -2123,7 +2134,7 @@ ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n
 }
 
 ShardGroup *group_create_hosted(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank,
-                                int device, const kh_transport *t, int exchange) {
+                                int device, const kh_transport *t, int mode) {
     if (world < 1 || world > 64) fail(KH_EVALUE, "group size must be in [1, 64]");
     if (rank < 0 || rank >= world) fail(KH_EVALUE, "invalid rank");
     if (!t->allgather || !t->broadcast || !t->alltoallv) fail(KH_EVALUE, "incomplete host transport");
@@ -2133,7 +2144,7 @@ ShardGroup *group_create_hosted(int kind, int hash, int k, const uint64_t *sizes
     G->rank0 = rank;
     G->hosted = true;
     G->tp = *t;
-    group_make_shards(G.get(), kind, hash, k, sizes, n, &device, exchange != 0);
+    group_make_shards(G.get(), kind, hash, k, sizes, n, &device, mode);
     G->loc.resize(1);
     KH_HIP(hipSetDevice(device));
     KH_HIP(hipMalloc((void **)&G->d_red, 256 * 8));
@@ -2658,10 +2669,13 @@ static PassState a2a_owner_pass(ShardGroup *G, int l, const std::vector<uint64_t
 
 // finalize of the own chunk (its k-mers are [r * stride, r * stride + nkc) of
 // the pass), counters, and the bigcount events of every rank merged into
-// every rank's map (ByteStorage::add's saturating sum is order-free)
+// every rank's map (ByteStorage::add's saturating sum is order-free).
+// on_views (delta mode): the chunk was applied on the rank's view, whose
+// per-k-mer full tallies and counters are complete for its own k-mers (index
+// 0 .. nkc); the counters still go to the shard.
 template <class Src>
 static void a2a_stage_c(ShardGroup *G, std::vector<PassState> &ps, const std::vector<Src> &srcs, uint64_t stride,
-                        uint64_t nkc) {
+                        uint64_t nkc, bool on_views = false) {
     const int W = G->world, NL = G->nlocal;
     std::vector<std::vector<uint64_t>> keys(W);
     std::vector<std::vector<uint32_t>> cnts(W);
@@ -2669,7 +2683,9 @@ static void a2a_stage_c(ShardGroup *G, std::vector<PassState> &ps, const std::ve
     const bool bigc = ps[0].bigc;
     for (int l = 0; l < NL; l++) {
         const int r = G->rank0 + l;
-        Graph *g = G->shards[l];
+        Graph *g = on_views ? G->views[l] : G->shards[l];
+        Graph *home = G->shards[l];
+        const uint64_t foff = on_views ? 0 : (uint64_t)r * stride;
         Workspace &w = g->ws;
         const Params &P = g->prm;
         hipStream_t st = g->stream;
@@ -2679,7 +2695,7 @@ static void a2a_stage_c(ShardGroup *G, std::vector<PassState> &ps, const std::ve
         for (;;) {
             if (bigc)
                 TIMED("finalize", hipLaunchKernelGGL(k_finalize<Src>, dim3(fgrid), dim3(FIN_THREADS), 0, st, P,
-                                                     srcs[l], nkc, w.fullf + (uint64_t)r * stride, w.ctr, w.bck, w.bcv,
+                                                     srcs[l], nkc, w.fullf + foff, w.ctr, w.bck, w.bcv,
                                                      w.cap_bcmap - 1, (uint64_t *)nullptr));
             KH_HIP(hipGetLastError());
             KH_HIP(hipMemcpyAsync(w.h_ctr, w.ctr, CTR_N * 8, hipMemcpyDeviceToHost, st));
@@ -2691,9 +2707,10 @@ static void a2a_stage_c(ShardGroup *G, std::vector<PassState> &ps, const std::ve
             KH_HIP(hipMemsetAsync(w.ctr + CTR_BCFF, 0, 8, st));
         }
         engine_collect_events(g);
+        if (on_views) move_kstats(home, g);
         if (w.h_ctr[CTR_ERR]) fail(KH_EDEVICE, "device pipeline error flag set");
-        g->n_occupied += w.h_ctr[CTR_OCC];
-        g->n_unique += w.h_ctr[CTR_UNIQUE];
+        home->n_occupied += w.h_ctr[CTR_OCC];
+        home->n_unique += w.h_ctr[CTR_UNIQUE];
         if (!bigc) continue;
         const uint64_t nkeys = w.h_ctr[CTR_NBC];
         nff[r] = w.h_ctr[CTR_BCFF];
@@ -2890,6 +2907,286 @@ static void group_consume_a2a(ShardGroup *G, const GroupReads &R) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Delta mode (KH_GROUP_DELTA, khmer_hip.h): per pass, every rank
+//   1. partitions its own chunk on its full-geometry view (single-GPU level 1
+//      and level 2, k-mer indices local to the chunk) and writes the chunk's
+//      delta tables D_r (k_apply_delta) into the view's arena;
+//   2. sends owner o the bytes of o's slice (all-to-all of table bytes);
+//   3. as owner, turns the W deltas of its slice into the prefixes
+//      P_r = T + D_0 + ... + D_{r-1} and its new slice T + D_0 + ... +
+//      D_{W-1} (k_delta_prefix, saturating in the storage's layout);
+//   4. receives its own prefix P_r of every slice back into the view's arena;
+//   5. applies its chunk over P_r with the single-GPU apply: a bin's value
+//      there is exactly what the stream (the rank chunks in rank order) shows
+//      when the rank's chunk begins, so the apply's is_new winners, table-0
+//      first touches and full inserts are the reference's for the rank's own
+//      k-mers (storage.hh:571-624, 320-359, 172-199) -- n_unique,
+//      n_occupied and bigcount events need no routing;
+//   6. finalize + counters + bigcount events merged (a2a_stage_c on views).
+// The view's arena then holds P_r plus its own inserts and is overwritten by
+// the next pass's delta.
+
+// bytes [*b0, *b0 + *nb) of table i's reference layout held by rank o: the
+// bytes of its bucket-aligned bin slice (bin slices start on byte
+// boundaries).  Only bytes that hold bins travel: a Bit / Nibble table's
+// trailing byte past its last bin (p/8 + 1, p/2 + 1 bytes of storage)
+// stays 0 on every rank.
+static void delta_slice(const ShardGroup *G, int o, int i, uint64_t *b0, uint64_t *nb) {
+    const Graph *V = G->views[0];
+    const int n = V->n;
+    const uint64_t lo = G->blo[(size_t)o * n + i], hi = G->bhi[(size_t)o * n + i];
+    const uint64_t bpb = V->kind == BIT ? 8 : V->kind == NIBBLE ? 2 : 1;   // bins per byte
+    *b0 = lo / bpb;
+    *nb = lo < hi ? (hi + bpb - 1) / bpb - *b0 : 0;
+}
+// owner o's delta buffer: W blocks of `stride` bytes (one per source rank),
+// table i's slice at offset soff[i] of a block (256-B aligned: the prefix
+// kernel's 16-B accesses)
+static uint64_t delta_layout(const ShardGroup *G, int o, std::vector<uint64_t> &soff) {
+    const int n = G->views[0]->n;
+    soff.assign(n, 0);
+    uint64_t acc = 0;
+    for (int i = 0; i < n; i++) {
+        uint64_t b0, nb;
+        delta_slice(G, o, i, &b0, &nb);
+        soff[i] = acc;
+        acc += (nb + 255) / 256 * 256;
+    }
+    return std::max<uint64_t>(acc, 256);
+}
+
+// step 1b: the chunk's delta tables into the view's arena
+static void delta_apply(Graph *V, PassState &ps, bool l2f) {
+    const Params &P = V->prm;
+    Workspace &w = V->ws;
+    ApplyArgs A{};
+    A.rlo = l2f ? w.reg_base : w.off2;
+    A.rhi = l2f ? w.reg_cur : w.off2 + 1;
+    A.rec = w.rec2;
+    A.tab = V->d_tab;
+    A.rprefix[0] = 0;
+    for (int i = 0; i < P.n; i++) A.rprefix[i + 1] = A.rprefix[i] + ((P.lsz[i] + (1ull << P.s0) - 1) >> P.s0);
+    const uint64_t total = A.rprefix[P.n];
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(total, 4 * device_cus(V)));
+    const int th = 1 << (P.s0 - 4);
+    const size_t lds = ((size_t)1 << P.s0) * 4;
+    hipStream_t st = V->stream;
+    Graph *g = V;
+    if (th == 1024) {
+        if (P.kind == BYTE) TIMED("apply_delta", hipLaunchKernelGGL((k_apply_delta<BYTE, 1024>), dim3(grid), dim3(1024), lds, st, P, A));
+        else if (P.kind == NIBBLE) TIMED("apply_delta", hipLaunchKernelGGL((k_apply_delta<NIBBLE, 1024>), dim3(grid), dim3(1024), lds, st, P, A));
+        else TIMED("apply_delta", hipLaunchKernelGGL((k_apply_delta<BIT, 1024>), dim3(grid), dim3(1024), lds, st, P, A));
+    } else {
+        if (P.kind == BYTE) TIMED("apply_delta", hipLaunchKernelGGL((k_apply_delta<BYTE, 512>), dim3(grid), dim3(512), lds, st, P, A));
+        else if (P.kind == NIBBLE) TIMED("apply_delta", hipLaunchKernelGGL((k_apply_delta<NIBBLE, 512>), dim3(grid), dim3(512), lds, st, P, A));
+        else TIMED("apply_delta", hipLaunchKernelGGL((k_apply_delta<BIT, 512>), dim3(grid), dim3(512), lds, st, P, A));
+    }
+    KH_HIP(hipGetLastError());
+    (void)ps;
+}
+
+// steps 2 and 4: forward = every rank's delta slices to their owners'
+// buffers; backward = every owner's prefix slices back into the ranks' views
+static void delta_exchange(ShardGroup *G, bool forward) {
+    const int W = G->world, NL = G->nlocal, n = G->views[0]->n;
+    std::vector<std::vector<uint64_t>> soff(W);
+    std::vector<uint64_t> stride(W);
+    for (int o = 0; o < W; o++) stride[o] = delta_layout(G, o, soff[o]);
+    auto slice = [&](int o, int i, uint64_t *b0, uint64_t *nb) { delta_slice(G, o, i, b0, nb); };
+    if (G->comm) {
+        Graph *V = G->views[0];
+        auto &lc = G->loc[0];
+        const int r = G->rank0;
+        KH_HIP(hipSetDevice(V->device));
+        hipStream_t st = V->stream;
+        // own slice: a device copy
+        for (int i = 0; i < n; i++) {
+            uint64_t b0, nb;
+            slice(r, i, &b0, &nb);
+            if (!nb) continue;
+            uint8_t *vt = V->d_tab + V->prm.tbyte[i] + b0;
+            uint8_t *bt = lc.dbuf + (uint64_t)r * stride[r] + soff[r][i];
+            KH_HIP(hipMemcpyAsync(forward ? bt : vt, forward ? vt : bt, nb, hipMemcpyDeviceToDevice, st));
+        }
+        KH_NCCL(ncclGroupStart());
+        for (int d = 0; d < W; d++) {
+            if (d == r) continue;
+            for (int i = 0; i < n; i++) {
+                uint64_t b0, nb;
+                if (forward) {
+                    slice(d, i, &b0, &nb);   // my delta of d's slice -> d
+                    if (nb) KH_NCCL(ncclSend(V->d_tab + V->prm.tbyte[i] + b0, nb, ncclUint8, d, G->comm, st));
+                    slice(r, i, &b0, &nb);   // d's delta of my slice
+                    if (nb) KH_NCCL(ncclRecv(lc.dbuf + (uint64_t)d * stride[r] + soff[r][i], nb, ncclUint8, d, G->comm, st));
+                } else {
+                    slice(r, i, &b0, &nb);   // d's prefix of my slice -> d
+                    if (nb) KH_NCCL(ncclSend(lc.dbuf + (uint64_t)d * stride[r] + soff[r][i], nb, ncclUint8, d, G->comm, st));
+                    slice(d, i, &b0, &nb);   // my prefix of d's slice
+                    if (nb) KH_NCCL(ncclRecv(V->d_tab + V->prm.tbyte[i] + b0, nb, ncclUint8, d, G->comm, st));
+                }
+            }
+        }
+        KH_NCCL(ncclGroupEnd());
+        return;
+    }
+    if (G->hosted) {
+        // one alltoallv; every (source, owner) block is the owner's padded
+        // layout, so a received block drops into the delta buffer as it is
+        Graph *V = G->views[0];
+        auto &lc = G->loc[0];
+        const int r = G->rank0;
+        KH_HIP(hipSetDevice(V->device));
+        hipStream_t st = V->stream;
+        std::vector<uint64_t> sb(W), rb(W), at(W + 1, 0);
+        for (int d = 0; d < W; d++) {
+            sb[d] = forward ? stride[d] : stride[r];
+            rb[d] = forward ? stride[r] : stride[d];
+            at[d + 1] = at[d] + sb[d];
+        }
+        std::vector<uint8_t> hs(at[W] + 1), hr;
+        KH_HIP(hipStreamSynchronize(st));
+        for (int d = 0; d < W; d++)
+            for (int i = 0; i < n; i++) {
+                uint64_t b0, nb;
+                if (forward) {
+                    slice(d, i, &b0, &nb);
+                    if (nb) KH_HIP(hipMemcpy(hs.data() + at[d] + soff[d][i], V->d_tab + V->prm.tbyte[i] + b0, nb,
+                                             hipMemcpyDeviceToHost));
+                } else {
+                    slice(r, i, &b0, &nb);
+                    if (nb) KH_HIP(hipMemcpy(hs.data() + at[d] + soff[r][i], lc.dbuf + (uint64_t)d * stride[r] + soff[r][i],
+                                             nb, hipMemcpyDeviceToHost));
+                }
+            }
+        uint64_t rtot = 0;
+        for (int d = 0; d < W; d++) rtot += rb[d];
+        hr.resize(rtot + 1);
+        host_rc(G->tp.alltoallv(G->tp.ctx, hs.data(), sb.data(), hr.data(), rb.data()), "alltoallv");
+        uint64_t q = 0;
+        for (int s = 0; s < W; s++) {
+            for (int i = 0; i < n; i++) {
+                uint64_t b0, nb;
+                if (forward) {
+                    slice(r, i, &b0, &nb);
+                    if (nb) KH_HIP(hipMemcpy(lc.dbuf + (uint64_t)s * stride[r] + soff[r][i], hr.data() + q + soff[r][i], nb,
+                                             hipMemcpyHostToDevice));
+                } else {
+                    slice(s, i, &b0, &nb);
+                    if (nb) KH_HIP(hipMemcpy(V->d_tab + V->prm.tbyte[i] + b0, hr.data() + q + soff[s][i], nb,
+                                             hipMemcpyHostToDevice));
+                }
+            }
+            q += rb[s];
+        }
+        return;
+    }
+    // loopback: device copies between the local views and owners
+    for (int l = 0; l < NL; l++) KH_HIP(hipStreamSynchronize(G->views[l]->stream));
+    for (int o = 0; o < W; o++) {
+        auto &lc = G->loc[o];
+        Graph *Vo = G->views[o];
+        KH_HIP(hipSetDevice(Vo->device));
+        for (int s = 0; s < W; s++) {
+            Graph *Vs = G->views[s];
+            for (int i = 0; i < n; i++) {
+                uint64_t b0, nb;
+                slice(o, i, &b0, &nb);
+                if (!nb) continue;
+                uint8_t *vt = Vs->d_tab + Vs->prm.tbyte[i] + b0;
+                uint8_t *bt = lc.dbuf + (uint64_t)s * stride[o] + soff[o][i];
+                KH_HIP(hipMemcpyAsync(forward ? bt : vt, forward ? vt : bt, nb, hipMemcpyDefault, Vo->stream));
+            }
+        }
+    }
+    for (int l = 0; l < NL; l++) KH_HIP(hipStreamSynchronize(G->views[l]->stream));
+}
+
+// step 3: the owner's prefixes and its new slice
+static void delta_prefix(ShardGroup *G, int l) {
+    const int W = G->world, r = G->rank0 + l;
+    Graph *g = G->shards[l];
+    Graph *V = G->views[l];
+    auto &lc = G->loc[l];
+    std::vector<uint64_t> soff;
+    const uint64_t stride = delta_layout(G, r, soff);
+    KH_HIP(hipSetDevice(g->device));
+    for (int i = 0; i < g->n; i++) {
+        uint64_t b0, nb;
+        delta_slice(G, r, i, &b0, &nb);
+        if (!nb) continue;
+        uint8_t *T = g->d_tab + g->prm.tbyte[i];
+        uint8_t *buf = lc.dbuf + soff[i];
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb + 16 * 256 - 1) / (16 * 256), 8192));
+        Graph *gt = V;   // timed on the view's stream (the pass's stream)
+        {
+            KTimer kt_(gt, "delta_prefix");
+            if (g->kind == BYTE)
+                hipLaunchKernelGGL(k_delta_prefix<BYTE>, dim3(grid), dim3(256), 0, V->stream, T, buf, nb, stride, W);
+            else if (g->kind == NIBBLE)
+                hipLaunchKernelGGL(k_delta_prefix<NIBBLE>, dim3(grid), dim3(256), 0, V->stream, T, buf, nb, stride, W);
+            else
+                hipLaunchKernelGGL(k_delta_prefix<BIT>, dim3(grid), dim3(256), 0, V->stream, T, buf, nb, stride, W);
+        }
+        KH_HIP(hipGetLastError());
+    }
+}
+
+// Delta-mode passes: up to the graph's batch (<= MAX_PASS_KMERS) of every
+// rank's own reads per pass (a2a_pass_plan at world 1;
+// khmer_amd.parallel.delta_passes restates it)
+template <class Src>
+static void group_consume_delta(ShardGroup *G, const GroupReads &R) {
+    const int W = G->world, NL = G->nlocal;
+    Graph *g0 = G->shards[0];
+    const uint64_t kpr = R.kpr, nreads = R.nreads;
+    const uint64_t cap = std::min<uint64_t>(g0->batch_kmers, MAX_PASS_KMERS);
+    const uint64_t rpb0 = std::max<uint64_t>(1, (cap > 16 ? cap - 16 : 1) / kpr);
+    const uint64_t npass = std::max<uint64_t>(1, (nreads + rpb0 - 1) / rpb0);
+    const uint64_t rpb = std::max<uint64_t>(1, (nreads + npass - 1) / npass);
+    GROUP_TRY(for (int l = 0; l < NL; l++) {
+        const int r = G->rank0 + l;
+        std::vector<uint64_t> soff;
+        const uint64_t stride = delta_layout(G, r, soff);
+        KH_HIP(hipSetDevice(G->shards[l]->device));
+        ensure((void **)&G->loc[l].dbuf, &G->loc[l].cap_dbuf, (uint64_t)W * stride, 1);
+    });
+    for (uint64_t r0 = 0; r0 < nreads; r0 += rpb) {
+        const uint64_t nr = std::min(rpb, nreads - r0), nkc = nr * kpr;
+        std::vector<Src> srcs(NL);
+        std::vector<PassState> ps(NL);
+        std::vector<char> fast(NL, 0);
+        GROUP_TRY(for (int l = 0; l < NL; l++) {
+            Graph *V = G->views[l];
+            Graph *sh = G->shards[l];
+            KH_HIP(hipSetDevice(V->device));
+            V->use_bigcount = sh->use_bigcount;
+            V->prm.use_bigcount = sh->prm.use_bigcount;
+            V->profile = sh->profile;
+            srcs[l] = group_src<Src>(V, R, R.d[l], r0, nr);
+            bool f = false;
+            ps[l] = pass_stage_a(V, srcs[l], nkc, false, &f);
+            fast[l] = f;
+            delta_apply(V, ps[l], f);
+        });
+        delta_exchange(G, true);
+        GROUP_TRY(for (int l = 0; l < NL; l++) delta_prefix(G, l));
+        delta_exchange(G, false);
+        GROUP_TRY(for (int l = 0; l < NL; l++) {
+            Graph *V = G->views[l];
+            KH_HIP(hipSetDevice(V->device));
+            pass_apply(V, ps[l], fast[l] != 0);
+            pass_mark_local(V, ps[l], false);
+        });
+        a2a_stage_c(G, ps, srcs, 0, nkc, true);
+    }
+    for (int l = 0; l < NL; l++) {
+        KH_HIP(hipSetDevice(G->shards[l]->device));
+        KH_HIP(hipStreamSynchronize(G->views[l]->stream));
+        KH_HIP(hipStreamSynchronize(G->shards[l]->stream));
+    }
+}
+
 // the broadcast-mode consume (Option B) of every rank's reads, source by source
 template <class Src>
 static void group_consume_bcast(ShardGroup *G, const GroupReads &R) {
@@ -3044,7 +3341,8 @@ static GroupReads group_reads(ShardGroup *G, bool bytes, const void *const *d, u
 void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len) {
     const GroupReads R = group_reads(G, false, (const void *const *)d_words, nreads, read_len);
     if (!nreads) return;
-    if (G->a2a) group_consume_a2a<SrcTwoBit>(G, R);
+    if (G->delta) group_consume_delta<SrcTwoBit>(G, R);
+    else if (G->a2a) group_consume_a2a<SrcTwoBit>(G, R);
     else group_consume_bcast<SrcTwoBit>(G, R);
 }
 
@@ -3052,7 +3350,8 @@ void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t
 void group_consume_bytes_fixed(ShardGroup *G, const uint8_t *const *d_bytes, uint64_t nreads, uint64_t read_len) {
     const GroupReads R = group_reads(G, true, (const void *const *)d_bytes, nreads, read_len);
     if (!nreads) return;
-    if (G->a2a) group_consume_a2a<SrcBytes>(G, R);
+    if (G->delta) group_consume_delta<SrcBytes>(G, R);
+    else if (G->a2a) group_consume_a2a<SrcBytes>(G, R);
     else group_consume_bcast<SrcBytes>(G, R);
 }
 
@@ -3345,7 +3644,7 @@ void group_rank_slice(ShardGroup *G, int rank, int table, uint64_t *lo, uint64_t
         *size = shard_lo(g->sizes[(size_t)table], G->world, rank + 1) - *lo;
     }
 }
-int group_exchange(ShardGroup *G) { return G->a2a ? 1 : 0; }
+int group_exchange(ShardGroup *G) { return G->delta ? 2 : G->a2a ? 1 : 0; }
 int group_world(ShardGroup *G) { return G->world; }
 int group_nlocal(ShardGroup *G) { return G->nlocal; }
 int group_rank(ShardGroup *G, int l) { return G->rank0 + l; }

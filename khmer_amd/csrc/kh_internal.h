@@ -378,11 +378,11 @@ void engine_collect_events(Graph *g);
 struct ShardGroup;
 void group_unique_id(unsigned char *out, size_t n);
 ShardGroup *group_create(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank, int nlocal,
-                         const int *devices, const unsigned char *uid, int exchange);
+                         const int *devices, const unsigned char *uid, int mode);   // mode: KH_GROUP_*
 ShardGroup *group_create_hosted(int kind, int hash, int k, const uint64_t *sizes, int n, int world, int rank,
-                                int device, const kh_transport *t, int exchange);
+                                int device, const kh_transport *t, int mode);
 void group_rank_slice(ShardGroup *G, int rank, int table, uint64_t *lo, uint64_t *size);
-int group_exchange(ShardGroup *G);
+int group_exchange(ShardGroup *G);   // the group's KH_GROUP_* mode
 void group_comm_info(ShardGroup *G, int *nranks, int *device);
 void group_destroy(ShardGroup *G);
 void group_consume_fixed(ShardGroup *G, const uint64_t *const *d_words, uint64_t nreads, uint64_t read_len);

@@ -88,6 +88,37 @@ def exchange_passes(nreads, read_len, k, world, batch_kmers):
     return [(r0, min(rpb, nreads - r0)) for r0 in range(0, nreads, rpb)]
 
 
+def delta_passes(nreads, read_len, k, batch_kmers):
+    """[(r0, nr)]: the passes a delta-mode group takes from every rank's
+    `nreads` reads (kh_engine.hip group_consume_delta): up to one device pass
+    of every rank's own reads, the rank chunks of a pass in rank order."""
+    return exchange_passes(nreads, read_len, k, 1, batch_kmers)
+
+
+def group_stream(mode, nreads, read_len, k, world, batch_kmers, step=None):
+    """[(first read, count)] of the whole group's stream in the order a
+    `mode` group consumes it, rank r holding reads [r * nreads, (r + 1) *
+    nreads): rank order (broadcast), or pass by pass with the rank chunks of a
+    pass in rank order (exchange: exchange_passes; delta: delta_passes).
+    `step` splits the pieces further (the oracle's batch size)."""
+    if mode == "broadcast":
+        plan = [(0, nreads)]
+    elif mode == "exchange":
+        plan = exchange_passes(nreads, read_len, k, world, batch_kmers)
+    elif mode == "delta":
+        plan = delta_passes(nreads, read_len, k, batch_kmers)
+    else:
+        raise ValueError("unknown group mode %r" % (mode,))
+    out = []
+    pieces = [(s * nreads + r0, nr) for r0, nr in plan for s in range(world)]
+    for a, n in pieces:
+        if step:
+            out += [(a + x, min(step, n - x)) for x in range(0, n, step)]
+        else:
+            out.append((a, n))
+    return out
+
+
 def window_owner_range(fj, world, r):
     """k-mer windows [lo, hi) whose winners rank r unions (kh_engine.hip group_wlo)."""
     return fj * r // world, fj * (r + 1) // world
@@ -208,7 +239,10 @@ class ShardedGraph(object):
     """A Countgraph/Nodegraph/SmallCountgraph split over `world` ranks."""
 
     def __init__(self, cls, k, sizes, world, rank=0, device=0, loopback=False, uid=None, transport=None,
-                 exchange=False):
+                 exchange=False, mode=None):
+        """mode: "broadcast" (Option B, the default), "exchange" (Option A;
+        also exchange=True) or "delta" (table deltas, include/khmer_hip.h
+        KH_GROUP_DELTA)."""
         self._h = None
         self.shards = []
         self.kind = KIND[cls]
@@ -221,8 +255,9 @@ class ShardedGraph(object):
         devs = (ctypes.c_int * nlocal)(*([device] * nlocal))
         arr = (ctypes.c_uint64 * len(sizes))(*self.sizes)
         h = ctypes.c_void_p()
-        mode = _lib.GROUP_EXCHANGE if exchange else _lib.GROUP_BROADCAST
-        self.exchange = bool(exchange)
+        self.mode = mode or ("exchange" if exchange else "broadcast")
+        mode = _lib.GROUP_MODES[self.mode]
+        self.exchange = self.mode != "broadcast"   # bucket-aligned ownership (exchange / delta)
         if transport is not None:
             check(lib.kh_group_create_hosted_mode(self.kind, hash_kind, k, arr, len(sizes), world, rank,
                                                   device, ctypes.byref(transport.struct), mode, ctypes.byref(h)))
@@ -370,8 +405,9 @@ class ShardedCountgraphBench(object):
         a = self.args
         return a.graph + " k=%d %dx%.0e sharded over %dxMI355X%s, %s%d x %d bp synthetic %sreads per GPU%s" % (
             a.k, a.tables, a.x, self.world,
-            " (exchange: each rank hashes its own reads, buckets sent to owners)" if getattr(a, "exchange", False)
-            else "", "get_median_count over " if a.query else "", a.reads, a.read_len,
+            {"exchange": " (exchange: each rank hashes its own reads, buckets sent to owners)",
+             "delta": " (delta: each rank counts its own reads, table deltas to owners, prefixes back)"}.get(
+                getattr(a, "group_mode", "broadcast"), ""), "get_median_count over " if a.query else "", a.reads, a.read_len,
             "genomic " if a.genome else "",
             " (strong scaling: %d reads in all)" % (a.reads * self.world) if a.strong else "")
 
@@ -385,13 +421,13 @@ class ShardedCountgraphBench(object):
         # and the rendezvous -- the dry run of several ranks on one device
         # (KH_BENCH_DEVICE), which RCCL refuses ("Duplicate GPU detected")
         self.transport = os.environ.get("KH_BENCH_TRANSPORT", "host" if "KH_BENCH_DEVICE" in os.environ else "rccl")
-        ex = bool(getattr(a, "exchange", False))
+        mode = getattr(a, "group_mode", "broadcast")
         if self.transport == "host":
             self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device,
-                                  transport=HostTransport(self.rdv), exchange=ex)
+                                  transport=HostTransport(self.rdv), mode=mode)
         else:
             uid = self.rdv.broadcast(ShardedGraph.unique_id() if self.rank == 0 else b"", 0)
-            self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device, uid=uid, exchange=ex)
+            self.g = ShardedGraph(a.graph, a.k, self.sizes, self.world, self.rank, self.device, uid=uid, mode=mode)
         nranks, dev = self.g.comm_info()
         self.comm = [tuple(int(x) for x in p.split(b",")) for p in
                      self.rdv.allgather(b"%d,%d,%d" % (self.rank, nranks, dev))]

@@ -16,6 +16,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <sys/mman.h>
 #include <string.h>
 #include <zlib.h>
 
@@ -257,8 +258,14 @@ or_table *or_table_new(int kind, int hash, int k, const uint64_t *sizes, int n) 
         t->nbytes[i] = kind == OR_BIT ? sizes[i] / 8 + 1 : kind == OR_NIBBLE ? sizes[i] / 2 + 1 : sizes[i];
         /* allocate + memset like the reference (storage.hh:502-511): pages are
          * touched at construction, not inside a timed consume */
-        t->tab[i] = malloc(t->nbytes[i] ? t->nbytes[i] : 1);
+        /* 2 MB aligned and backed by transparent huge pages where the kernel
+         * allows it: a GB table's random adds miss the TLB on 4 KB pages */
+        void *mem = NULL;
+        const size_t want = t->nbytes[i] ? t->nbytes[i] : 1;
+        if (posix_memalign(&mem, (size_t)2 << 20, want) != 0) mem = NULL;
+        t->tab[i] = mem;
         if (!t->tab[i]) { set_err("out of memory"); or_table_free(t); return NULL; }
+        if (want >= ((size_t)2 << 20)) madvise(mem, want, MADV_HUGEPAGE);
         memset(t->tab[i], 0, t->nbytes[i] ? t->nbytes[i] : 1);
         for (uint64_t b = 0; b < t->nbytes[i]; b += 4096) ((volatile uint8_t *)t->tab[i])[b] = 0;
     }
@@ -286,11 +293,16 @@ void or_bigcount_export(const or_table *t, uint64_t *keys, uint16_t *vals) {
     for (uint64_t i = 0; i < j; i++) vals[i] = t->bigcounts.vals[map_find(&t->bigcounts, keys[i])];
 }
 
+/* bins of hash h: bin_i = h % p_i (storage.hh:177, 321, 576) */
+static inline void bins_of(const or_table *t, uint64_t h, uint64_t *bins) {
+    for (int i = 0; i < t->n; i++) bins[i] = h % t->sizes[i];
+}
+
 /* BitStorage::test_and_set_bits: include/oxli/storage.hh:172-199 */
-static int bit_add(or_table *t, uint64_t h) {
+static int bit_add_b(or_table *t, const uint64_t *bins) {
     int is_new = 0;
     for (int i = 0; i < t->n; i++) {
-        uint64_t bin = h % t->sizes[i];
+        uint64_t bin = bins[i];
         uint8_t bit = (uint8_t)(1u << (bin % 8));
         uint8_t orig = t->tab[i][bin / 8];
         t->tab[i][bin / 8] = orig | bit;
@@ -304,10 +316,10 @@ static int bit_add(or_table *t, uint64_t h) {
 }
 
 /* NibbleStorage::add: include/oxli/storage.hh:320-359 (even bin -> high nibble) */
-static int nibble_add(or_table *t, uint64_t h) {
+static int nibble_add_b(or_table *t, const uint64_t *bins) {
     int is_new = 0;
     for (int i = 0; i < t->n; i++) {
-        uint64_t bin = h % t->sizes[i];
+        uint64_t bin = bins[i];
         uint64_t idx = bin / 2;
         uint8_t mask = (bin % 2) ? 0x0F : 0xF0;
         int shift = (bin % 2) ? 0 : 4;
@@ -325,11 +337,11 @@ static int nibble_add(or_table *t, uint64_t h) {
 }
 
 /* ByteStorage::add: include/oxli/storage.hh:571-624 */
-static int byte_add(or_table *t, uint64_t h) {
+static int byte_add_b(or_table *t, uint64_t h, const uint64_t *bins) {
     int is_new = 0;
     int n_full = 0;
     for (int i = 0; i < t->n; i++) {
-        uint64_t bin = h % t->sizes[i];
+        uint64_t bin = bins[i];
         uint8_t cur = t->tab[i][bin];
         if (!is_new && cur == 0) {
             is_new = 1;
@@ -348,12 +360,23 @@ static int byte_add(or_table *t, uint64_t h) {
     return is_new;
 }
 
-int or_add(or_table *t, uint64_t h) {
+static int add_b(or_table *t, uint64_t h, const uint64_t *bins) {
     switch (t->kind) {
-    case OR_BIT: return bit_add(t, h);
-    case OR_NIBBLE: return nibble_add(t, h);
-    default: return byte_add(t, h);
+    case OR_BIT: return bit_add_b(t, bins);
+    case OR_NIBBLE: return nibble_add_b(t, bins);
+    default: return byte_add_b(t, h, bins);
     }
+}
+static int bit_add(or_table *t, uint64_t h) {
+    uint64_t b[64];
+    bins_of(t, h, b);
+    return bit_add_b(t, b);
+}
+
+int or_add(or_table *t, uint64_t h) {
+    uint64_t b[64];
+    bins_of(t, h, b);
+    return add_b(t, h, b);
 }
 
 /* get_count: storage.hh:206-219 (bit), :362-379 (nibble), :627-649 (byte) */
@@ -985,15 +1008,42 @@ void or_synth_genomic_read(uint64_t seed, uint64_t G, uint64_t r, int L, char *o
 }
 
 /* consume reads r0..r0+nreads-1 of a synthetic stream in stream order
- * (genome == 0: iid uniform stream; otherwise the genomic stream) */
+ * (genome == 0: iid uniform stream; otherwise the genomic stream).  The
+ * k-mers of a group of reads are hashed and binned first, then added one by
+ * one in stream order (the same add as or_consume_string) while the table
+ * bytes of the k-mer PF_AHEAD places later are prefetched: GB tables make
+ * every add a cache miss, and the golden fixtures run 5e10 adds. */
+struct sink_h { uint64_t *h; uint64_t n; };
+static void cb_sink(void *ctx, uint64_t h) { struct sink_h *s = ctx; s->h[s->n++] = h; }
+#define PF_GROUP 64
+#define PF_AHEAD 24
 uint64_t or_consume_synth(or_table *t, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L) {
     char *buf = malloc((size_t)L + 1);
+    const int n = t->n;
+    const uint64_t cap = (uint64_t)PF_GROUP * (uint64_t)(L + 1);
+    uint64_t *hs = malloc(cap * 8), *bins = malloc(cap * (uint64_t)n * 8);
+    const int shift = t->kind == OR_BIT ? 3 : t->kind == OR_NIBBLE ? 1 : 0;
     uint64_t total = 0;
-    for (uint64_t r = r0; r < r0 + nreads; r++) {
-        if (genome) or_synth_genomic_read(seed, genome, r, L, buf);
-        else or_synth_read(seed, r, L, buf);
-        total += or_consume_string(t, buf, (size_t)L);
+    for (uint64_t g = r0; g < r0 + nreads; g += PF_GROUP) {
+        const uint64_t ge = g + PF_GROUP < r0 + nreads ? g + PF_GROUP : r0 + nreads;
+        struct sink_h sk = {hs, 0};
+        for (uint64_t r = g; r < ge; r++) {
+            if (genome) or_synth_genomic_read(seed, genome, r, L, buf);
+            else or_synth_read(seed, r, L, buf);
+            iterate_kmers(t, buf, (size_t)L, cb_sink, &sk);
+        }
+        for (uint64_t j = 0; j < sk.n; j++) bins_of(t, hs[j], bins + j * (uint64_t)n);
+        for (uint64_t j = 0; j < sk.n; j++) {
+            if (j + PF_AHEAD < sk.n) {
+                const uint64_t *b = bins + (j + PF_AHEAD) * (uint64_t)n;
+                for (int i = 0; i < n; i++) __builtin_prefetch(t->tab[i] + (b[i] >> shift), 1, 0);
+            }
+            add_b(t, hs[j], bins + j * (uint64_t)n);
+        }
+        total += sk.n;
     }
+    free(hs);
+    free(bins);
     free(buf);
     return total;
 }

@@ -81,21 +81,35 @@ EXCHANGE = {
 for _name, (_base, _world, _batch) in EXCHANGE.items():
     CONFIGS[_name] = dict(CONFIGS[_base], exchange=[_world, _batch])
 
+# Delta-mode (KH_GROUP_DELTA) streams: passes of up to `batch_kmers` k-mers of
+# every rank's reads, the rank chunks of a pass in rank order
+# (khmer_amd.parallel.delta_passes); n_unique and the bigcount map follow it.
+DELTA = {
+    # bench.py --gpus G (weak scaling, the default group mode and batch): the
+    # driver's scaling lines
+    "c2_w2_d": ("c2_w2", 2, 3200 << 20),
+    "c2_w4_d": ("c2_w4", 4, 3200 << 20),
+    "c2_w8_d": ("c2_w8", 8, 3200 << 20),
+    # loopback tests (tests/test_gpu_shard.py): several passes per rank
+    "c2_full_d2": ("c2_full", 2, 1600 << 20),
+    "genomic_c2_d2": ("genomic_c2", 2, 1 << 28),
+    "c4_shape_d2": ("c4_shape", 2, 1 << 28),
+    "c5m_genomic_d2": ("c5m_genomic", 2, 1 << 25),
+}
+for _name, (_base, _world, _batch) in DELTA.items():
+    CONFIGS[_name] = dict(CONFIGS[_base], delta=[_world, _batch])
+
 
 def stream_chunks(c, step=1_000_000):
     """[(r0, nreads)] in the order the configuration's stream consumes them:
-    the reads in order, or the exchange-mode pass interleave."""
-    if "exchange" not in c:
-        return [(r0, min(step, c["reads"] - r0)) for r0 in range(0, c["reads"], step)]
-    from khmer_amd.parallel import exchange_passes
-    world, batch = c["exchange"]
-    per = c["reads"] // world
-    out = []
-    for r0, nr in exchange_passes(per, c["L"], c["k"], world, batch):
-        for s in range(world):
-            for a in range(0, nr, step):
-                out.append((s * per + r0 + a, min(step, nr - a)))
-    return out
+    the reads in order, or a group mode's pass interleave
+    (khmer_amd.parallel.group_stream)."""
+    from khmer_amd.parallel import group_stream
+    for mode in ("exchange", "delta"):
+        if mode in c:
+            world, batch = c[mode]
+            return group_stream(mode, c["reads"] // world, c["L"], c["k"], world, batch, step=step)
+    return [(r0, min(step, c["reads"] - r0)) for r0 in range(0, c["reads"], step)]
 
 
 def sha256_view(mv, chunk=1 << 28):

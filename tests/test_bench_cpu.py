@@ -43,10 +43,10 @@ def test_exchange_fixture_order(bench):
     order (c2_full_x2b: 2 ranks at the default batch) is an exact match; with
     none for the order (8 ranks at the default batch) the rank-order fixture
     checks the order-free outputs only."""
-    a = _args(bench, ["--gpus", "2", "--strong"])
-    fx, exact = bench.matching_fixture(a, 50_000_000, [2, a.batch_kmers])
+    a = _args(bench, ["--gpus", "2", "--strong", "--group-mode", "exchange"])
+    fx, exact = bench.matching_fixture(a, 50_000_000, ("exchange", [2, a.batch_kmers]))
     assert fx["config"] == "c2_full_x2b" and exact
-    fx, exact = bench.matching_fixture(a, 50_000_000, [8, a.batch_kmers])
+    fx, exact = bench.matching_fixture(a, 50_000_000, ("exchange", [8, a.batch_kmers]))
     assert fx["config"] == "c2_full" and not exact
     part = bench.compare_fixture(fx, 1, fx["n_occupied"], fx["table_sha256"], stream_order=False)
     assert part["n_occupied_match"] and part["tables_match"] and "counters_match" not in part

@@ -35,8 +35,7 @@ def _rank_main():
     _lib.set_default_device(0)
     rdv = Rendezvous(rank, world, "127.0.0.1", int(os.environ["KH_RDV_PORT"]), timeout=120)
     tp = parallel.HostTransport(rdv)
-    g = parallel.ShardedGraph(cfg["cls"], cfg["k"], cfg["sizes"], world, rank, 0, transport=tp,
-                              exchange=cfg.get("exchange", False))
+    g = parallel.ShardedGraph(cfg["cls"], cfg["k"], cfg["sizes"], world, rank, 0, transport=tp, mode=cfg["mode"])
     g.set_batch_kmers(cfg["batch"])
     if cfg["bigcount"]:
         g.set_use_bigcount(True)
@@ -101,10 +100,16 @@ def _free_port():
                           ("Nodegraph", 2, False, True, False),
                           # the Counttable family and the sharded get_median_count (round 4)
                           ("SmallCounttable", 2, False, False, True), ("SmallCounttable", 3, False, True, True),
-                          ("Counttable", 2, True, True, True), ("Countgraph", 3, True, False, True)])
+                          ("Counttable", 2, True, True, True), ("Countgraph", 3, True, False, True),
+                          # delta mode (round 5): table-byte alltoallv both ways
+                          ("Countgraph", 2, True, "delta", False), ("Countgraph", 3, True, "delta", True),
+                          ("Nodegraph", 2, False, "delta", False), ("SmallCountgraph", 3, False, "delta", False),
+                          ("SmallCounttable", 2, False, "delta", True)])
 def test_hosted_group_multiprocess(cls, world, bigcount, exchange, query):
     """exchange=True: Option A through the host transport's alltoallv (the
-    oracle consumes the pass-interleaved stream, parallel.exchange_passes).
+    oracle consumes the pass-interleaved stream, parallel.exchange_passes);
+    exchange="delta": delta mode (table-byte alltoallv to the owners and
+    back, parallel.delta_passes).
     query=True: every rank's get_median_count of its own reads through the
     host transport's MIN reduce (broadcast) / reduce-scatter (exchange),
     against the oracle's per-read (median, average, stddev) bit patterns."""
@@ -118,8 +123,9 @@ def test_hosted_group_multiprocess(cls, world, bigcount, exchange, query):
     # bigcount cases read a 6 kbp genome (every k-mer ~400x, past 255 in all
     # tables); the query cases a 40 kbp genome; the others the iid stream
     genome = 6000 if bigcount else 40000 if query else 0
+    mode = "delta" if exchange == "delta" else "exchange" if exchange else "broadcast"
     cfg = {"cls": cls, "k": k, "sizes": sizes, "batch": 1 << 20, "bigcount": bigcount, "nreads": 20000, "L": 150,
-           "genome": genome, "exchange": exchange, "query": query}
+           "genome": genome, "mode": mode, "query": query}
     port = _free_port()
     procs = []
     for r in range(world):
@@ -140,8 +146,7 @@ def test_hosted_group_multiprocess(cls, world, bigcount, exchange, query):
     o = O.Table(KINDS[cls], k, sizes, hash=O.MURMUR if murmur else O.TWOBIT)
     o.set_use_bigcount(bigcount)
     n = cfg["nreads"]
-    order = ([(s * n + r0, nr) for r0, nr in parallel.exchange_passes(n, cfg["L"], k, world, cfg["batch"])
-              for s in range(world)] if exchange else [(s * n, n) for s in range(world)])
+    order = parallel.group_stream(mode, n, cfg["L"], k, world, cfg["batch"])
     for start, cnt in order:
         if genome:
             seqs, offs = synth.genomic_batch(start, cnt, cfg["L"], genome)
