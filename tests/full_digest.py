@@ -94,7 +94,6 @@ DELTA = {
     "c2_full_d2": ("c2_full", 2, 1600 << 20),
     "genomic_c2_d2": ("genomic_c2", 2, 1 << 28),
     "c4_shape_d2": ("c4_shape", 2, 1 << 28),
-    "c5m_genomic_d2": ("c5m_genomic", 2, 1 << 25),
 }
 for _name, (_base, _world, _batch) in DELTA.items():
     CONFIGS[_name] = dict(CONFIGS[_base], delta=[_world, _batch])
