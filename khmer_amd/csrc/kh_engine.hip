@@ -230,7 +230,9 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
     if (w.reg_base && w.reg_nkmers == nkmers && w.reg_sigma == g->cap_sigma) return w.reg_total;
     const uint64_t nreg = (uint64_t)P.F1 << P.s2;
     const uint64_t R = 1ull << P.s0;
-    const uint64_t slack = (uint64_t)(l2f_parts(P.F1) + 1) * (1ull << l2f_blk_sh()) + 16;
+    // every writing workgroup's partially filled block and its spare block
+    // (k_scatter_l2f), one more block and the 16-record alignment
+    const uint64_t slack = (uint64_t)(2 * l2f_parts(P.F1) + 1) * (1ull << l2f_blk_sh()) + 16;
     std::vector<uint64_t> base(nreg + 1, 0);
     uint64_t acc = 0;
     int i = 0;

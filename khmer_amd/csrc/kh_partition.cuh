@@ -457,7 +457,7 @@ constexpr int L1F_BLK_SH = 8;   // default block: 256 records (KH_L1F_BLK_SH)
 // other arrays (lds_scatter_l1f adds 2 * L1F_TW words)
 constexpr int L1F_TW = 128;
 __host__ __device__ constexpr size_t l1f_tw_offset(size_t F1a, int rpt) {
-    // u64 index: 5 F1a u64 arrays, then (stage u32 + sb u16 + sj u16) per
+    // u64 index: 5 F1a u64 arrays, then one u64 slot per
     // record, 5 F1a u32 arrays, s_wtot, s_meta, s_koff (the window, unused
     // for fixed-length reads) rounded to 8 bytes
     return (F1a * 8 * 5 + ((size_t)L1_THREADS * rpt + 2 * F1a) * 8 + F1a * 4 * 5 + 64 + 16 + 7) / 8;
@@ -485,14 +485,17 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
     // and one trailing pad (every bucket's run starts on an even slot, so
     // stage slot pairs map onto 16-B aligned output record pairs)
     const uint32_t NSLOT = TILE_RECS + 2 * F1a;
-    uint32_t *stage = (uint32_t *)(tail + F1a);         // [NSLOT] bin offset inside the bucket
-    uint32_t *cnt = stage + NSLOT;                      // [F1] records appended by this workgroup
+    // one 8-byte slot per staged record: (bucket << 16 | k-mer index in the
+    // tile) << 32 | bin offset inside the bucket (index SLOT_EMPTY: hole /
+    // pad); 16-B aligned (5 F1a u64 arrays before it, F1a a multiple of 4),
+    // so a slot pair is one 16-byte LDS read in the write-out
+    uint64_t *slot = tail + F1a;                        // [NSLOT]
+    uint32_t *cnt = (uint32_t *)(slot + NSLOT);         // [F1] records appended by this workgroup
     uint32_t *hist = cnt + F1a;                         // [F1]
-    uint32_t *lstart = hist + F1a;                      // [F1]
+    uint32_t *lstart = hist + F1a;                      // [F1] the bucket's first record slot of the tile
     uint2 *qq = (uint2 *)(lstart + F1a);                // [F1] (first LDS position in the new blocks,
                                                         //       first LDS position left for the tail)
-    uint32_t *sbj = (uint32_t *)(qq + F1a);             // [NSLOT] bucket << 16 | k-mer index in the tile (SLOT_EMPTY: hole / pad)
-    uint32_t *s_wtot = sbj + NSLOT;                     // [16]
+    uint32_t *s_wtot = (uint32_t *)(qq + F1a);          // [16]
     constexpr uint32_t SLOT_EMPTY = 0xFFFFu;
     uint64_t *s_meta = (uint64_t *)(s_wtot + 16);
     uint64_t *s_koff = s_meta + 2;
@@ -642,6 +645,8 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             const uint32_t h = hist[d];
             return h ? (h + (cnt[d] & 1u) + 1u) & ~1u : 0u;
         };
+        // lstart[d] = the run's first record slot: its region start plus
+        // the leading hole (staging then reads one LDS word per record)
         if (F1 > 256) {
             // many buckets: every thread scans two (F1 <= 2 * L1_THREADS),
             // wave totals through s_wtot (one more barrier)
@@ -657,28 +662,35 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             block_sync();
             uint32_t acc = incl - r0 - r1;
             for (uint32_t w = 0; w < wave; w++) acc += s_wtot[w];
-            if (d0 < F1) lstart[d0] = acc;
-            if (d0 + 1 < F1) lstart[d0 + 1] = acc + r0;
+            if (d0 < F1) lstart[d0] = acc + (cnt[d0] & 1u);
+            if (d0 + 1 < F1) lstart[d0 + 1] = acc + r0 + (cnt[d0 + 1] & 1u);
         } else if (threadIdx.x < 64) {
-            // <= 4 buckets a lane, unrolled: the lane's LDS reads issue back
-            // to back and the run sizes stay in registers for the writes
-            const uint32_t lane = threadIdx.x, per = (F1 + 63) / 64, b0 = lane * per;
-            uint32_t rs[4], sum = 0;
+            // rows of 64 buckets: lane l holds buckets l, 64 + l, 128 + l and
+            // 192 + l (conflict-free LDS reads); four independent wave scans,
+            // then the rows' totals
+            const uint32_t lane = threadIdx.x;
+            uint32_t rs[4], incl[4], par[4];
 #pragma unroll
             for (uint32_t t = 0; t < 4; t++) {
-                rs[t] = (t < per && b0 + t < F1) ? run(b0 + t) : 0u;
-                sum += rs[t];
+                const uint32_t d = 64 * t + lane;
+                const uint32_t h = d < F1 ? hist[d] : 0u;
+                par[t] = d < F1 ? (cnt[d] & 1u) : 0u;
+                rs[t] = h ? (h + par[t] + 1u) & ~1u : 0u;
+                incl[t] = rs[t];
             }
-            uint32_t incl = sum;
             for (int dd = 1; dd < 64; dd <<= 1) {
-                const uint32_t y = __shfl_up(incl, dd, 64);
-                if (lane >= (uint32_t)dd) incl += y;
+#pragma unroll
+                for (uint32_t t = 0; t < 4; t++) {
+                    const uint32_t y = __shfl_up(incl[t], dd, 64);
+                    if (lane >= (uint32_t)dd) incl[t] += y;
+                }
             }
-            uint32_t acc = incl - sum;
+            uint32_t base = 0;
 #pragma unroll
             for (uint32_t t = 0; t < 4; t++) {
-                if (t < per && b0 + t < F1) lstart[b0 + t] = acc;
-                acc += rs[t];
+                const uint32_t d = 64 * t + lane;
+                if (d < F1) lstart[d] = base + incl[t] - rs[t] + par[t];
+                base += __shfl(incl[t], 63, 64);
             }
         }
         block_sync();
@@ -687,9 +699,8 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
         for (int q = 0; q < RPT; q++) {
             if (off[q] != ~0u) {
                 const uint32_t b = (br[q] >> 13) & 1023u;
-                const uint32_t pos = lstart[b] + (cnt[b] & 1u) + (br[q] & 8191u);
-                stage[pos] = off[q];
-                sbj[pos] = (b << 16) | ((br[q] >> 23) * L1_THREADS + threadIdx.x);
+                const uint32_t pos = lstart[b] + (br[q] & 8191u);
+                slot[pos] = (uint64_t)((b << 16) | ((br[q] >> 23) * L1_THREADS + threadIdx.x)) << 32 | off[q];
             }
         }
         // The next tile's packed words go to their LDS buffer here, not after
@@ -731,10 +742,10 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             }
             const uint32_t e = L0 + h, fe = last ? e : (e & ~1u);
             if ((L0 & 1) && fe > L0 - 1 && bc != DEAD) rec[bc + ((L0 - 1) & (BLK - 1))] = tail[d];
-            const uint32_t q0 = lstart[d] + (L0 & 1);   // the run's first slot (odd after a hole)
+            const uint32_t q0 = lstart[d];   // the run's first slot (odd after a hole)
             if (h) {
-                if (L0 & 1) sbj[q0 - 1] = (d << 16) | SLOT_EMPTY;
-                if ((q0 + h) & 1) sbj[q0 + h] = (d << 16) | SLOT_EMPTY;
+                if (L0 & 1) slot[q0 - 1] = (uint64_t)((d << 16) | SLOT_EMPTY) << 32;
+                if ((q0 + h) & 1) slot[q0 + h] = (uint64_t)((d << 16) | SLOT_EMPTY) << 32;
             }
             const bool dead = bc == DEAD || nb == DEAD;
             nbase[d] = nb;
@@ -753,9 +764,9 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
         // bucket's tail when it is the run's unpaired last (not on the last tile)
         {
             const uint32_t dlast = F1 - 1;
-            const uint32_t nslot = lstart[dlast] + (hist[dlast] ? (hist[dlast] + (cnt[dlast] & 1u) + 1u) & ~1u : 0u);
-            const uint2 *sbj2 = (const uint2 *)sbj;
-            const uint2 *stage2 = (const uint2 *)stage;
+            const uint32_t pl = cnt[dlast] & 1u;
+            const uint32_t nslot = lstart[dlast] - pl + (hist[dlast] ? (hist[dlast] + pl + 1u) & ~1u : 0u);
+            const ulonglong2 *slot2 = (const ulonglong2 *)slot;
             const ulonglong2 *dl2 = (const ulonglong2 *)dl;   // both placement constants in one 16-B read
             auto put_pair = [&](uint32_t m, uint2 bj, uint2 st, uint2 ql, ulonglong2 dd) {
                 const uint32_t q = 2 * m;
@@ -773,35 +784,12 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
                     tail[d] = v0;   // the run's unpaired last record
                 }
             };
-#ifdef KH_L1_WO_BATCH
-            // development: WU pairs per thread per step, their LDS reads issued together
-            constexpr int WU = KH_L1_WO_BATCH;
-            for (uint32_t m0 = threadIdx.x; 2 * m0 < nslot; m0 += WU * L1_THREADS) {
-                uint2 bj[WU], st[WU], ql[WU];
-                ulonglong2 dd[WU];
-#pragma unroll
-                for (int u = 0; u < WU; u++) {
-                    const uint32_t m = m0 + (uint32_t)u * L1_THREADS;
-                    const bool ok = 2 * m < nslot;
-                    bj[u] = ok ? sbj2[m] : make_uint2(SLOT_EMPTY, SLOT_EMPTY);
-                    st[u] = ok ? stage2[m] : make_uint2(0, 0);
-                }
-#pragma unroll
-                for (int u = 0; u < WU; u++) {
-                    const uint32_t d = bj[u].x >> 16;
-                    ql[u] = qq[d];
-                    dd[u] = dl2[d];
-                }
-#pragma unroll
-                for (int u = 0; u < WU; u++) put_pair(m0 + (uint32_t)u * L1_THREADS, bj[u], st[u], ql[u], dd[u]);
-            }
-#else
             for (uint32_t m = threadIdx.x; 2 * m < nslot; m += L1_THREADS) {
-                const uint2 bj = sbj2[m];
+                const ulonglong2 sp = slot2[m];
+                const uint2 bj = make_uint2((uint32_t)(sp.x >> 32), (uint32_t)(sp.y >> 32));
                 const uint32_t d = bj.x >> 16;
-                put_pair(m, bj, stage2[m], qq[d], dl2[d]);
+                put_pair(m, bj, make_uint2((uint32_t)sp.x, (uint32_t)sp.y), qq[d], dl2[d]);
             }
-#endif
         }
         PH(6);
         block_sync();
@@ -1391,8 +1379,21 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2(uint32_t F1, int s0, int
 // [reg_base[g], reg_cur[g]).  A reservation past the region's capacity (a
 // skewed input) sets ctr[CTR_ERR] bit 4, writes nothing for that region, and
 // the host redoes the pass's level 2 with the exact histogram path.
+//
+// Spare blocks (round 5): a reservation is a returning global atomic, and
+// waiting for it every tile put its round trip on the critical path (the
+// "reserve" phase, ~25 % of the kernel).  Thread d (region d) now keeps one
+// spare block of its region in a register, reserved one tile ahead once the
+// current block has fewer than L2F_SPARE_LOW free slots; a tile that needs
+// exactly one new block takes the spare (no wait) and the next spare's atomic
+// overlaps the tile's flushes and stores.  The next tile's record loads are
+// issued after the reservations, so waiting for a spare never waits for them.
+// An unused spare is filled with sentinels at the end (reg_plan's slack holds
+// one more block per workgroup and region).
 constexpr int L2F_BLK_SH = 6;   // default block: 64 records (KH_L2F_BLK_SH)
 constexpr uint64_t L2F_DEAD = ~0ull;
+constexpr uint64_t L2F_NONE = ~1ull;   // no spare block
+constexpr uint32_t L2F_SPARE_LOW = 16;
 
 template <int THREADS, int RPT>
 __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, int s2, uint32_t parts,
@@ -1453,6 +1454,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
     load_tile(r0, v);
     PH_BEGIN(8);
     const uint32_t ntiles = uniform_u32((uint32_t)((r1 - r0 + TILE - 1) / TILE));
+    uint64_t spare = L2F_NONE;   // thread d: a reserved, unused block of region d
     for (uint32_t ti = 0; ti < ntiles; ti++) {
         const uint64_t t0 = r0 + (uint64_t)ti * TILE;
         const bool last = ti + 1 == ntiles;
@@ -1466,7 +1468,6 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
             if (x[q] != ~0ull) rank[q] = atomicAdd(&hist[(uint32_t)x[q] >> s0], 1u);
         }
         PH(0);
-        load_tile(t0 + TILE, v);
         block_sync();
         PH(1);
         // blocks for this tile (one reservation per region that needs any) and
@@ -1489,6 +1490,11 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
                     const uint32_t need = ((c0 + h + BLK - 1) >> blk_sh) - ((c0 + BLK - 1) >> blk_sh);
                     if (dead) {
                         nb = L2F_DEAD;
+                    } else if (need == 1 && spare != L2F_NONE) {
+                        nb = spare;   // reserved a tile or more ago: no wait
+                        spare = L2F_NONE;
+                        nlim = reg_base[gb + d + 1];
+                        nneed = 1;
                     } else if (need) {
                         nb = atomicAdd(&reg_cur[gb + d], (unsigned long long)need * BLK);
                         nlim = reg_base[gb + d + 1];
@@ -1502,6 +1508,13 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
                 }
                 nbase[d] = nb;
 #endif
+                // the next spare: once this tile leaves fewer than
+                // L2F_SPARE_LOW free slots in the region's current block
+                // (not on the last tile; never for an overflowed region)
+                const uint32_t e1 = c0 + h;
+                const uint32_t free_after = (BLK - (e1 & (BLK - 1))) & (BLK - 1);
+                if (!last && !dead && nb != L2F_DEAD && spare == L2F_NONE && e1 > 0 && free_after < L2F_SPARE_LOW)
+                    spare = atomicAdd(&reg_cur[gb + d], (unsigned long long)BLK);
                 const uint32_t a = c0 & ~(SEG - 1), e = c0 + h;
                 fl = !dead && c0 != a && (last ? e : (e & ~(SEG - 1))) > a;
             }
@@ -1513,6 +1526,9 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
                 if (fl) flist[base + (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63)) - 1))] = (uint16_t)d;
             }
         }
+        // the next tile's records: after the reservations, so the wait for a
+        // spare (next tile) never includes these loads
+        load_tile(t0 + TILE, v);
         PH(2);
         block_sync();
         PH(3);
@@ -1567,13 +1583,23 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
         }
     }
     PH_END(32, 8);
-    // the rest of every partially filled block: sentinels
+    // the rest of every partially filled block: sentinels; an unused spare
+    // (a whole block, past the region's capacity when it overflowed): sentinels
     block_sync();
     for (uint32_t y = threadIdx.x; y < F2 * BLK; y += THREADS) {
         const uint32_t d = y >> blk_sh, sl = y & (BLK - 1);
         const uint32_t c = cnt[d] & (BLK - 1);
         if (c == 0 || sl < c || bcur[d] == L2F_DEAD) continue;
         rec_out[bcur[d] + sl] = ~0ull;
+    }
+    if (threadIdx.x < F2 && spare != L2F_NONE) {
+        const uint32_t d = threadIdx.x;
+        if (spare + BLK <= reg_base[gb + d + 1]) {
+            for (uint32_t sl = 0; sl < BLK; sl += 2)
+                *(ulonglong2 *)(rec_out + spare + sl) = make_ulonglong2(~0ull, ~0ull);
+        } else {
+            atomicOr((unsigned long long *)&ctr[CTR_ERR], 4ull);
+        }
     }
 }
 

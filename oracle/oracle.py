@@ -253,6 +253,15 @@ class Table:
     def n_occupied(self):
         return lib().or_n_occupied(self._h)
 
+    def set_table_bytes(self, i, data):
+        """Overwrite table i's bytes (the storage half of Hashtable::load,
+        src/oxli/storage.cc:272-404; counters are left as they are)."""
+        n = lib().or_table_nbytes(self._h, i)
+        if len(data) != n:
+            raise ValueError("table %d holds %d bytes, got %d" % (i, n, len(data)))
+        p = lib().or_table_data(self._h, i)
+        ctypes.memmove(ctypes.addressof(p.contents), bytes(data), n)
+
     def table_bytes(self, i):
         n = lib().or_table_nbytes(self._h, i)
         p = lib().or_table_data(self._h, i)
