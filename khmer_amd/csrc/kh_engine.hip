@@ -767,6 +767,15 @@ static uint64_t own_filter(Graph *g, const Src &src, uint64_t nkmers, bool windo
 
 // k_scatter_l1f over every level-1 window (l1f_windows) of graph g's
 // geometry: records of k-mer j carry index jbase + j
+// the software-pipelined level 1 (k_scatter_l1p): a -DKH_L1_PIPE build
+// (A/B against k_scatter_l1f)
+static bool l1p_on() {
+#ifdef KH_L1_PIPE
+    return true;
+#else
+    return false;
+#endif
+}
 template <class Src>
 static void launch_l1f(Graph *g, const Src &src, uint64_t nkmers, bool window, uint32_t jbase) {
     Workspace &w = g->ws;
@@ -779,6 +788,17 @@ static void launch_l1f(Graph *g, const Src &src, uint64_t nkmers, bool window, u
         const uint64_t tk = (uint64_t)L1_THREADS * kpt;
         const uint64_t kpw = (nkmers + (uint64_t)nwg * tk - 1) / ((uint64_t)nwg * tk) * tk;
         KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, g->stream));   // the chunk queue's head
+        if constexpr (std::is_same<Src, SrcTwoBit>::value) {
+            if (l1p_on() && !window && l1f_tw(src, kpt) && Q.F1 <= 256 && l1f_chunk_tiles(g) >= 1 && kpt == 2 &&
+                rpt == L1_MAX_RPT) {
+                const size_t lds = lds_l1p((Q.F1 + 3) & ~3u, rpt);
+                TIMED("scatter_l1", hipLaunchKernelGGL(k_scatter_l1p<2>, dim3(nwg), dim3(L1_THREADS), lds, g->stream, Q,
+                                                       src, nkmers, kpw, wn.t0, wn.nt, w.bkt_base + wn.bb0,
+                                                       (unsigned long long *)w.bkt_cur + wn.bb0, w.rec1, w.ctr,
+                                                       l1f_blk_sh(), jbase, l1f_chunk_tiles(g)));
+                continue;
+            }
+        }
         TIMED("scatter_l1", hipLaunchKernelGGL(l1f_kernel<Src>(kpt, rpt, !window && l1f_tw(src, kpt)), dim3(nwg),
                                                dim3(L1_THREADS), lds_scatter_l1f(Q, window, (int)tk), g->stream, Q,
                                                src, nkmers, kpw, wn.t0, wn.nt, w.bkt_base + wn.bb0,
@@ -797,7 +817,7 @@ static bool recs_fit(Graph *g, uint64_t nkmers, double sigma) {
     double recs = 0;
     for (int i = 0; i < P.n; i++) {
         const double regions = (double)P.lsz[i] / R, mean = (double)nkmers * R / (double)P.p[i];
-        recs += regions * (mean + sigma * sqrt(mean) + (double)((l2f_parts(P.F1) + 1) << l2f_blk_sh()));
+        recs += regions * (mean + sigma * sqrt(mean) + (double)((2 * l2f_parts(P.F1) + 1) << l2f_blk_sh()));
     }
     size_t freeb = 0, total = 0;
     if (hipMemGetInfo(&freeb, &total) != hipSuccess) return false;
@@ -1807,6 +1827,13 @@ static void set_lds_limits() {
     KH_LDS_MAX((k_own_filter<SrcHashes, 8>));
     KH_LDS_MAX((k_own_filter<SrcHashes, 16>));
     KH_LDS_MAX((k_scatter_w<PT_THREADS, 2>));
+    KH_LDS_MAX((k_scatter_l1p<2>));
+    KH_LDS_MAX((k_apply_delta<BYTE, 1024>));
+    KH_LDS_MAX((k_apply_delta<NIBBLE, 1024>));
+    KH_LDS_MAX((k_apply_delta<BIT, 1024>));
+    KH_LDS_MAX((k_apply_delta<BYTE, 512>));
+    KH_LDS_MAX((k_apply_delta<NIBBLE, 512>));
+    KH_LDS_MAX((k_apply_delta<BIT, 512>));
 #undef KH_LDS_MAX
     (void)hipFuncSetAttribute((const void *)k_mark, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_mark_wf, hipFuncAttributeMaxDynamicSharedMemorySize, lim);

@@ -825,6 +825,284 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
 }
 
 // ---------------------------------------------------------------------------
+// Software-pipelined k_scatter_l1f (round 5) for the hot case: fixed-length
+// 2-bit reads whose tile's packed words are staged in LDS, at most 256
+// buckets, dynamic chunks of >= 2 tiles.  k_scatter_l1f runs a tile as five
+// barrier-separated phases (rank | scan | stage | write-out | advance); here
+// a tile takes three, and the write-out of tile t shares its phase with the
+// hash + LDS rank of tile t + 1 (two tile histograms), so a wave that is done
+// writing moves on to hashing instead of waiting at a barrier, and the
+// tile's stores drain while the next tile is hashed:
+//   P1: block reservations, run-start scan (tile t)
+//   P2: staging, per-bucket placement constants and the bucket state
+//       advanced for tile t; the next tile's words into LDS
+//   P3: write-out of tile t, then hash + rank of tile t + 1
+// Records, blocks, holes and pads are exactly k_scatter_l1f's.
+template <int KPT>
+__global__ void __launch_bounds__(L1_THREADS, L1F_WAVES_PER_EU) k_scatter_l1p(Params P, SrcTwoBit src, uint64_t nkmers,
+                                                                             uint64_t kpw, int t0, int nt,
+                                                                             const uint64_t *bkt_base,
+                                                                             unsigned long long *bkt_cur, uint64_t *rec,
+                                                                             uint64_t *ctr, int blk_sh, uint32_t jbase,
+                                                                             uint32_t cht) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int RPT = L1_MAX_RPT;
+    constexpr int TILE_RECS = L1_THREADS * RPT;
+    constexpr int TILE_KMERS = L1_THREADS * KPT;
+    constexpr uint32_t SLOT_EMPTY = 0xFFFFu;
+    constexpr uint64_t DEAD = ~0ull;
+    (void)kpw;
+    const uint32_t BLK = 1u << blk_sh;
+    const uint32_t F1 = P.F1;
+    const uint32_t F1a = (F1 + 3) & ~3u;
+    const uint32_t NSLOT = TILE_RECS + 2 * F1a;
+    uint64_t *s_tw = (uint64_t *)smem;                  // [2][L1F_TW] packed words of the next tiles
+    uint64_t *bcur = s_tw + 2 * L1F_TW;                 // [F1] partially filled block (DEAD: overflowed)
+    uint64_t *nbase = bcur + F1a;                       // [F1] blocks reserved for the staged tile
+    uint64_t *dl = nbase + F1a;                         // [F1][2] output - LDS position
+    uint64_t *tail = dl + 2 * F1a;                      // [F1] a pending odd record
+    uint64_t *slot = tail + F1a;                        // [NSLOT] as in k_scatter_l1f
+    uint32_t *cnt = (uint32_t *)(slot + NSLOT);         // [F1] records appended by this workgroup
+    uint32_t *hist2 = cnt + F1a;                        // [2][F1] the tile histograms (tile parity)
+    uint32_t *lstart = hist2 + 2 * F1a;                 // [F1] the bucket's first record slot
+    uint2 *qq = (uint2 *)(lstart + F1a);                // [F1]
+    uint32_t *s_misc = (uint32_t *)(qq + F1a);          // [0] queue chunk, [1] slots of the staged tile
+    const int shift = P.s0 + P.s2;
+    const uint64_t omask = (1ull << shift) - 1;
+    for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) {
+        bcur[b] = 0;
+        cnt[b] = 0;
+        hist2[b] = 0;
+        hist2[F1a + b] = 0;
+    }
+    // the hash stage's tile iterator (k_scatter_l1f's chunk queue: workgroup
+    // w starts with chunks w and w + gridDim.x and takes one more from the
+    // queue on the first tile of every chunk; with >= 2 tiles a chunk, a
+    // queue result is published (P2) before the iterator needs it)
+    const uint64_t CK = (uint64_t)cht * TILE_KMERS;
+    const uint32_t nchunks = (uint32_t)((nkmers + CK - 1) / CK);
+    uint32_t cb = blockIdx.x + gridDim.x;
+    uint64_t hj0 = min(nkmers, (uint64_t)blockIdx.x * CK);   // the hashed tile's first k-mer
+    uint64_t hce = min(nkmers, hj0 + CK);                      // its chunk's end
+    bool htop = true;                                         // the hashed tile starts a chunk
+    auto tile_w0 = [&](uint64_t j0) -> uint64_t {
+        const uint64_t ja = j0 + src.kbase;
+        return ((ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2) >> 6;
+    };
+    auto tile_nw = [&](uint64_t j0, uint64_t j1) -> uint32_t { return (uint32_t)(tile_w0(j1 - 1) + 2 - tile_w0(j0)); };
+    // the tile after the hashed one: [*n0, *n1), empty when there is none
+    auto next_tile = [&](uint64_t j1, uint64_t *n0, uint64_t *n1) {
+        *n0 = j1;
+        *n1 = j1;
+        if (j1 < hce) {
+            *n1 = min(hce, j1 + TILE_KMERS);
+        } else if (cb < nchunks) {
+            *n0 = (uint64_t)cb * CK;
+            *n1 = min(nkmers, *n0 + (uint64_t)TILE_KMERS);
+        }
+    };
+    uint32_t off[RPT], br[RPT];
+    unsigned long long qn = 0;
+    uint64_t tw_next = 0;
+    // hash + rank of tile [j0, j1) into histogram h (words in s_tw[buf]); the
+    // next tile's words (nn0, nn1) are loaded into tw_next
+    auto hash_rank = [&](uint64_t j0, uint64_t j1, uint32_t *h, uint32_t buf) {
+#pragma unroll
+        for (int q = 0; q < RPT; q++) { off[q] = ~0u; br[q] = 0; }
+        const uint64_t *tw_cur = s_tw + buf * L1F_TW;
+        const uint64_t tw_w0 = tile_w0(j0);
+        uint64_t hh[KPT];
+#pragma unroll
+        for (int a = 0; a < KPT; a++) {
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            uint64_t x = 0;
+            if (j < j1) {
+                const uint64_t ja = j + src.kbase;
+                const uint64_t bpos = (ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2;
+                const uint32_t wi = (uint32_t)((bpos >> 6) - tw_w0);
+                x = src.finish(SrcTwoBit::Pend{tw_cur[wi], tw_cur[wi + 1], (uint32_t)(bpos & 63)});
+            }
+            hh[a] = x;
+        }
+#pragma unroll
+        for (int a = 0; a < KPT; a++) {
+            const uint64_t j = j0 + (uint64_t)a * L1_THREADS + threadIdx.x;
+            const bool ok = j < j1;
+#pragma unroll
+            for (int q = 0; q < RPT; q++) {
+                const int i = q - a * nt;
+                if (ok && i >= 0 && i < nt) {
+                    uint64_t Gq;
+                    if (local_bin(P, t0 + i, hh[a], &Gq)) {
+                        const uint32_t b = (uint32_t)(Gq >> shift);
+                        off[q] = (uint32_t)(Gq & omask);
+                        br[q] = ((uint32_t)a << 23) | (b << 13) | atomicAdd(&h[b], 1u);
+                    }
+                }
+            }
+        }
+    };
+    // prologue: the first tile's words, its queue atomic, hash + rank
+    uint64_t hj1 = min(hce, hj0 + TILE_KMERS);
+    if (hce > hj0 && threadIdx.x < tile_nw(hj0, hj1)) s_tw[threadIdx.x] = src.words[tile_w0(hj0) + threadIdx.x];
+    if (hce > hj0 && threadIdx.x == 0) qn = atomicAdd((unsigned long long *)&ctr[CTR_L1Q], 1ull);
+    block_sync();
+    uint64_t n0, n1;
+    next_tile(hj1, &n0, &n1);
+    if (hce > hj0) {
+        if (n1 > n0 && threadIdx.x < tile_nw(n0, n1)) tw_next = src.words[tile_w0(n0) + threadIdx.x];
+        hash_rank(hj0, hj1, hist2, 0);
+    }
+    block_sync();
+    for (uint32_t ti = 0; hce > hj0; ti++) {
+        // the staged tile (= the hashed one until P3 moves the iterator on)
+        const uint64_t j0 = hj0;
+        const bool last = n1 == n0;
+        const bool top = htop;
+        uint32_t *hist = hist2 + (ti & 1) * F1a;
+        // ---- P1: block reservations (thread d owns bucket d), run starts
+        uint64_t rsv = 0;
+        const uint32_t d = threadIdx.x;
+        if (d < F1 && bcur[d] != DEAD) {
+            const uint32_t h = hist[d], L0 = cnt[d];
+            const uint32_t need = ((L0 + h + BLK - 1) >> blk_sh) - (((L0 + BLK - 1) & ~(BLK - 1)) >> blk_sh);
+            if (need) rsv = atomicAdd(&bkt_cur[d], (unsigned long long)need * BLK);
+        }
+        if (threadIdx.x < 64) {
+            // rows of 64 buckets (conflict-free), four wave scans; lstart =
+            // the run's first record slot (region start + leading hole)
+            const uint32_t lane = threadIdx.x;
+            uint32_t rs[4], incl[4], par[4];
+#pragma unroll
+            for (uint32_t t = 0; t < 4; t++) {
+                const uint32_t b = 64 * t + lane;
+                const uint32_t h = b < F1 ? hist[b] : 0u;
+                par[t] = b < F1 ? (cnt[b] & 1u) : 0u;
+                rs[t] = h ? (h + par[t] + 1u) & ~1u : 0u;
+                incl[t] = rs[t];
+            }
+            for (int dd = 1; dd < 64; dd <<= 1) {
+#pragma unroll
+                for (uint32_t t = 0; t < 4; t++) {
+                    const uint32_t y = __shfl_up(incl[t], dd, 64);
+                    if (lane >= (uint32_t)dd) incl[t] += y;
+                }
+            }
+            uint32_t base = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < 4; t++) {
+                const uint32_t b = 64 * t + lane;
+                if (b < F1) lstart[b] = base + incl[t] - rs[t] + par[t];
+                base += __shfl(incl[t], 63, 64);
+            }
+            if (lane == 0) s_misc[1] = base;   // slots of the tile (even)
+        }
+        block_sync();
+        // ---- P2: staging; placement constants; bucket state advanced
+#pragma unroll
+        for (int q = 0; q < RPT; q++) {
+            if (off[q] != ~0u) {
+                const uint32_t b = (br[q] >> 13) & 1023u;
+                const uint32_t pos = lstart[b] + (br[q] & 8191u);
+                slot[pos] = (uint64_t)((b << 16) | ((br[q] >> 23) * L1_THREADS + threadIdx.x)) << 32 | off[q];
+            }
+        }
+        if (!last && threadIdx.x < L1F_TW) s_tw[((ti + 1) & 1) * L1F_TW + threadIdx.x] = tw_next;
+        if (top && threadIdx.x == 0) s_misc[0] = (uint32_t)min<unsigned long long>(qn + 2ull * gridDim.x, nchunks);
+        if (d < F1) {
+            const uint32_t h = hist[d];
+            if (h || last) {
+                const uint32_t L0 = cnt[d];
+                const uint32_t split = (L0 + BLK - 1) & ~(BLK - 1);
+                const uint32_t need = ((L0 + h + BLK - 1) >> blk_sh) - (split >> blk_sh);
+                const uint64_t bc = bcur[d];
+                uint64_t nb = 0;
+                if (bc == DEAD) {
+                    nb = DEAD;
+                } else if (need) {
+                    nb = rsv;
+                    if (nb + (uint64_t)need * BLK > bkt_base[d + 1]) {
+                        atomicOr((unsigned long long *)&ctr[CTR_ERR], 8ull);
+                        nb = DEAD;
+                    }
+                }
+                const uint32_t e = L0 + h, fe = last ? e : (e & ~1u);
+                if ((L0 & 1) && fe > L0 - 1 && bc != DEAD) rec[bc + ((L0 - 1) & (BLK - 1))] = tail[d];
+                const uint32_t q0 = lstart[d];
+                if (h) {
+                    if (L0 & 1) slot[q0 - 1] = (uint64_t)((d << 16) | SLOT_EMPTY) << 32;
+                    if ((q0 + h) & 1) slot[q0 + h] = (uint64_t)((d << 16) | SLOT_EMPTY) << 32;
+                }
+                const bool dead = bc == DEAD || nb == DEAD;
+                dl[2 * d] = bc + (L0 & (BLK - 1)) - q0;
+                dl[2 * d + 1] = nb + L0 - split - q0;
+                qq[d] = make_uint2(q0 + (split - L0), dead ? 0 : q0 + (fe > L0 ? fe - L0 : 0));
+                // the bucket's state after this tile (the write-out below reads
+                // only dl / qq / slot, and tail for unpaired last records)
+                if (h) {
+                    if (nb == DEAD) bcur[d] = DEAD;
+                    else if (need) bcur[d] = nb + (uint64_t)(need - 1) * BLK;
+                    cnt[d] = e;
+                    hist[d] = 0;
+                }
+            }
+        }
+        block_sync();
+        // ---- P3: write-out of the staged tile
+        {
+            const uint32_t nslot = s_misc[1];
+            const ulonglong2 *slot2 = (const ulonglong2 *)slot;
+            const ulonglong2 *dl2 = (const ulonglong2 *)dl;
+            for (uint32_t m = threadIdx.x; 2 * m < nslot; m += L1_THREADS) {
+                const ulonglong2 sp = slot2[m];
+                const uint32_t bj0 = (uint32_t)(sp.x >> 32), bj1 = (uint32_t)(sp.y >> 32);
+                const uint32_t dd = bj0 >> 16;
+                const uint2 ql = qq[dd];
+                const ulonglong2 dv = dl2[dd];
+                const uint32_t q = 2 * m;
+                const bool r0 = (bj0 & 0xFFFFu) != SLOT_EMPTY, r1 = (bj1 & 0xFFFFu) != SLOT_EMPTY;
+                const uint64_t v0 = ((jbase + j0 + (bj0 & 0xFFFFu)) << 32) | (uint32_t)sp.x;
+                const uint64_t v1 = ((jbase + j0 + (bj1 & 0xFFFFu)) << 32) | (uint32_t)sp.y;
+                const uint64_t o = (q >= ql.x ? dv.y : dv.x) + q;
+                if (q < ql.y) {
+                    if (r0 && r1) *(ulonglong2 *)(rec + o) = make_ulonglong2(v0, v1);
+                    else if (r0) rec[o] = v0;
+                    else if (r1) rec[o + 1] = v1;
+                } else if (r0) {
+                    tail[dd] = v0;
+                }
+            }
+        }
+        // ---- P3: the iterator moves on; hash + rank of the next tile
+        if (last) break;
+        if (hj1 >= hce) {   // into chunk cb (its successor published in P2 of its predecessor's top tile)
+            hce = min(nkmers, (uint64_t)cb * CK + CK);
+            cb = uniform_u32(s_misc[0]);
+            htop = true;
+        } else {
+            htop = false;
+        }
+        hj0 = n0;
+        hj1 = n1;
+        next_tile(hj1, &n0, &n1);
+        if (htop && threadIdx.x == 0) qn = atomicAdd((unsigned long long *)&ctr[CTR_L1Q], 1ull);
+        if (n1 > n0 && threadIdx.x < tile_nw(n0, n1)) tw_next = src.words[tile_w0(n0) + threadIdx.x];
+        hash_rank(hj0, hj1, hist2 + ((ti + 1) & 1) * F1a, (ti + 1) & 1);
+        block_sync();
+    }
+    block_sync();
+    for (uint32_t y = threadIdx.x; y < F1 * BLK; y += blockDim.x) {
+        const uint32_t dd = y >> blk_sh, sl = y & (BLK - 1);
+        const uint32_t c = cnt[dd] & (BLK - 1);
+        if (c == 0 || sl < c || bcur[dd] == DEAD) continue;
+        rec[bcur[dd] + sl] = ~0ull;
+    }
+}
+__host__ __device__ constexpr size_t lds_l1p(size_t F1a, int rpt) {
+    return 2 * L1F_TW * 8 + F1a * 8 * 5 + ((size_t)L1_THREADS * rpt + 2 * F1a) * 8 + F1a * 4 * 6 + 16;
+}
+
+// ---------------------------------------------------------------------------
 // Level 1 of a shard ("owned filter").  A shard of a G-rank group owns ~1/G
 // of every table's bins but hashes every k-mer of the stream, so with
 // k_hist_l1 + k_scatter_l1 it would hash each k-mer twice and run the whole

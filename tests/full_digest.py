@@ -90,6 +90,9 @@ DELTA = {
     "c2_w2_d": ("c2_w2", 2, 3200 << 20),
     "c2_w4_d": ("c2_w4", 4, 3200 << 20),
     "c2_w8_d": ("c2_w8", 8, 3200 << 20),
+    # the bench's multi-rank dry run on one GPU (KH_BENCH_DEVICE, host
+    # transport): two ranks' buffers on one device need a smaller batch
+    "c2_w2_d800": ("c2_w2", 2, 800 << 20),
     # loopback tests (tests/test_gpu_shard.py): several passes per rank
     "c2_full_d2": ("c2_full", 2, 1600 << 20),
     "genomic_c2_d2": ("genomic_c2", 2, 1 << 28),

@@ -34,8 +34,32 @@ def test_default_workload_is_c2_full(bench):
     # strong scaling over 8 ranks is the same stream (broadcast mode: rank order)
     a8 = _args(bench, ["--gpus", "8", "--strong", "--group-mode", "broadcast"])
     assert bench.matching_fixture(a8, 8 * ((a8.reads + 7) // 8)) == (bench.matching_fixture(a, a.reads)[0], True)
-    # weak scaling at 8 ranks: 400M reads, no fixture
-    assert bench.matching_fixture(a8, 8 * a8.reads) == (None, False)
+
+
+def _have(name):
+    from tests import full_digest as FD
+    return os.path.exists(FD.fixture_path(name))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_weak_scaling_lines_have_fixtures(bench, world):
+    """every `bench.py --gpus G` line the driver runs (C2, weak
+    scaling, 50M reads per rank, the default delta mode and batch) matches a
+    fixture made in its own stream order, so the line carries counters_match
+    and tables_match; other group modes fall back to the same reads in
+    another order (tables and n_occupied)."""
+    name = "c2_w%d_d" % world
+    if not _have(name):
+        pytest.skip("fixture %s not generated yet" % name)
+    a = _args(bench, ["--gpus", str(world)])
+    assert a.group_mode == "delta"
+    fx, exact = bench.matching_fixture(a, world * a.reads, (a.group_mode, [world, a.batch_kmers]))
+    assert fx["config"] == name and exact
+    assert fx["params"]["reads"] == world * 50_000_000
+    ax = _args(bench, ["--gpus", str(world), "--group-mode", "exchange"])
+    fx, exact = bench.matching_fixture(ax, world * ax.reads, ("exchange", [world, ax.batch_kmers]))
+    assert fx is not None and fx["params"]["reads"] == world * 50_000_000
+    assert exact == (fx["config"] == "c2_w%d_x" % world)
 
 
 def test_exchange_fixture_order(bench):
