@@ -230,9 +230,7 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
     if (w.reg_base && w.reg_nkmers == nkmers && w.reg_sigma == g->cap_sigma) return w.reg_total;
     const uint64_t nreg = (uint64_t)P.F1 << P.s2;
     const uint64_t R = 1ull << P.s0;
-    // every writing workgroup's partially filled block and its spare block
-    // (k_scatter_l2f), one more block and the 16-record alignment
-    const uint64_t slack = (uint64_t)(2 * l2f_parts(P.F1) + 1) * (1ull << l2f_blk_sh()) + 16;
+    const uint64_t slack = (uint64_t)(l2f_parts(P.F1) + 1) * (1ull << l2f_blk_sh()) + 16;
     std::vector<uint64_t> base(nreg + 1, 0);
     uint64_t acc = 0;
     int i = 0;
@@ -767,14 +765,13 @@ static uint64_t own_filter(Graph *g, const Src &src, uint64_t nkmers, bool windo
 
 // k_scatter_l1f over every level-1 window (l1f_windows) of graph g's
 // geometry: records of k-mer j carry index jbase + j
-// the software-pipelined level 1 (k_scatter_l1p): a -DKH_L1_PIPE build
-// (A/B against k_scatter_l1f)
+// the software-pipelined level 1 (k_scatter_l1p) for fixed-length 2-bit
+// reads at <= 256 buckets: 240.6 against 242.2 ms/step (k_scatter_l1f with
+// the same fused stage slots) and 243.4 (round 4's kernel), same box,
+// profiles/r5/ab_3way_b.txt; KH_L1F=1 keeps k_scatter_l1f (development)
 static bool l1p_on() {
-#ifdef KH_L1_PIPE
-    return true;
-#else
-    return false;
-#endif
+    static const bool off = env_seg("KH_L1F", 0) != 0;
+    return !off;
 }
 template <class Src>
 static void launch_l1f(Graph *g, const Src &src, uint64_t nkmers, bool window, uint32_t jbase) {
@@ -817,7 +814,7 @@ static bool recs_fit(Graph *g, uint64_t nkmers, double sigma) {
     double recs = 0;
     for (int i = 0; i < P.n; i++) {
         const double regions = (double)P.lsz[i] / R, mean = (double)nkmers * R / (double)P.p[i];
-        recs += regions * (mean + sigma * sqrt(mean) + (double)((2 * l2f_parts(P.F1) + 1) << l2f_blk_sh()));
+        recs += regions * (mean + sigma * sqrt(mean) + (double)((l2f_parts(P.F1) + 1) << l2f_blk_sh()));
     }
     size_t freeb = 0, total = 0;
     if (hipMemGetInfo(&freeb, &total) != hipSuccess) return false;

@@ -665,32 +665,27 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
             if (d0 < F1) lstart[d0] = acc + (cnt[d0] & 1u);
             if (d0 + 1 < F1) lstart[d0 + 1] = acc + r0 + (cnt[d0 + 1] & 1u);
         } else if (threadIdx.x < 64) {
-            // rows of 64 buckets: lane l holds buckets l, 64 + l, 128 + l and
-            // 192 + l (conflict-free LDS reads); four independent wave scans,
-            // then the rows' totals
-            const uint32_t lane = threadIdx.x;
-            uint32_t rs[4], incl[4], par[4];
+            // <= 4 buckets a lane, unrolled: the lane's LDS reads issue back
+            // to back and the run sizes stay in registers for the writes
+            // (four independent row scans over buckets l, 64 + l, ... spilled
+            // registers and measured 1 ms/step slower)
+            const uint32_t lane = threadIdx.x, per = (F1 + 63) / 64, b0 = lane * per;
+            uint32_t rs[4], sum = 0;
 #pragma unroll
             for (uint32_t t = 0; t < 4; t++) {
-                const uint32_t d = 64 * t + lane;
-                const uint32_t h = d < F1 ? hist[d] : 0u;
-                par[t] = d < F1 ? (cnt[d] & 1u) : 0u;
-                rs[t] = h ? (h + par[t] + 1u) & ~1u : 0u;
-                incl[t] = rs[t];
+                rs[t] = (t < per && b0 + t < F1) ? run(b0 + t) : 0u;
+                sum += rs[t];
             }
+            uint32_t incl = sum;
             for (int dd = 1; dd < 64; dd <<= 1) {
-#pragma unroll
-                for (uint32_t t = 0; t < 4; t++) {
-                    const uint32_t y = __shfl_up(incl[t], dd, 64);
-                    if (lane >= (uint32_t)dd) incl[t] += y;
-                }
+                const uint32_t y = __shfl_up(incl, dd, 64);
+                if (lane >= (uint32_t)dd) incl += y;
             }
-            uint32_t base = 0;
+            uint32_t acc = incl - sum;
 #pragma unroll
             for (uint32_t t = 0; t < 4; t++) {
-                const uint32_t d = 64 * t + lane;
-                if (d < F1) lstart[d] = base + incl[t] - rs[t] + par[t];
-                base += __shfl(incl[t], 63, 64);
+                if (t < per && b0 + t < F1) lstart[b0 + t] = acc + (cnt[b0 + t] & 1u);
+                acc += rs[t];
             }
         }
         block_sync();
@@ -858,8 +853,7 @@ __global__ void __launch_bounds__(L1_THREADS, L1F_WAVES_PER_EU) k_scatter_l1p(Pa
     const uint32_t NSLOT = TILE_RECS + 2 * F1a;
     uint64_t *s_tw = (uint64_t *)smem;                  // [2][L1F_TW] packed words of the next tiles
     uint64_t *bcur = s_tw + 2 * L1F_TW;                 // [F1] partially filled block (DEAD: overflowed)
-    uint64_t *nbase = bcur + F1a;                       // [F1] blocks reserved for the staged tile
-    uint64_t *dl = nbase + F1a;                         // [F1][2] output - LDS position
+    uint64_t *dl = bcur + F1a;                          // [F1][2] output - LDS position
     uint64_t *tail = dl + 2 * F1a;                      // [F1] a pending odd record
     uint64_t *slot = tail + F1a;                        // [NSLOT] as in k_scatter_l1f
     uint32_t *cnt = (uint32_t *)(slot + NSLOT);         // [F1] records appended by this workgroup
@@ -1099,7 +1093,7 @@ __global__ void __launch_bounds__(L1_THREADS, L1F_WAVES_PER_EU) k_scatter_l1p(Pa
     }
 }
 __host__ __device__ constexpr size_t lds_l1p(size_t F1a, int rpt) {
-    return 2 * L1F_TW * 8 + F1a * 8 * 5 + ((size_t)L1_THREADS * rpt + 2 * F1a) * 8 + F1a * 4 * 6 + 16;
+    return 2 * L1F_TW * 8 + F1a * 8 * 4 + ((size_t)L1_THREADS * rpt + 2 * F1a) * 8 + F1a * 4 * 6 + 16;
 }
 
 // ---------------------------------------------------------------------------
@@ -1658,20 +1652,12 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2(uint32_t F1, int s0, int
 // skewed input) sets ctr[CTR_ERR] bit 4, writes nothing for that region, and
 // the host redoes the pass's level 2 with the exact histogram path.
 //
-// Spare blocks (round 5): a reservation is a returning global atomic, and
-// waiting for it every tile put its round trip on the critical path (the
-// "reserve" phase, ~25 % of the kernel).  Thread d (region d) now keeps one
-// spare block of its region in a register, reserved one tile ahead once the
-// current block has fewer than L2F_SPARE_LOW free slots; a tile that needs
-// exactly one new block takes the spare (no wait) and the next spare's atomic
-// overlaps the tile's flushes and stores.  The next tile's record loads are
-// issued after the reservations, so waiting for a spare never waits for them.
-// An unused spare is filled with sentinels at the end (reg_plan's slack holds
-// one more block per workgroup and region).
+// (Round 5 measured spare blocks reserved one tile ahead -- each thread
+// keeping a reserved block of its region in a register so a tile rarely
+// waits for its reservation atomic: 93.7 against 90.1 ms/step on one box,
+// VGPRs 94 -> 102; not kept)
 constexpr int L2F_BLK_SH = 6;   // default block: 64 records (KH_L2F_BLK_SH)
 constexpr uint64_t L2F_DEAD = ~0ull;
-constexpr uint64_t L2F_NONE = ~1ull;   // no spare block
-constexpr uint32_t L2F_SPARE_LOW = 16;
 
 template <int THREADS, int RPT>
 __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, int s2, uint32_t parts,
@@ -1732,7 +1718,6 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
     load_tile(r0, v);
     PH_BEGIN(8);
     const uint32_t ntiles = uniform_u32((uint32_t)((r1 - r0 + TILE - 1) / TILE));
-    uint64_t spare = L2F_NONE;   // thread d: a reserved, unused block of region d
     for (uint32_t ti = 0; ti < ntiles; ti++) {
         const uint64_t t0 = r0 + (uint64_t)ti * TILE;
         const bool last = ti + 1 == ntiles;
@@ -1746,6 +1731,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
             if (x[q] != ~0ull) rank[q] = atomicAdd(&hist[(uint32_t)x[q] >> s0], 1u);
         }
         PH(0);
+        load_tile(t0 + TILE, v);
         block_sync();
         PH(1);
         // blocks for this tile (one reservation per region that needs any) and
@@ -1768,11 +1754,6 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
                     const uint32_t need = ((c0 + h + BLK - 1) >> blk_sh) - ((c0 + BLK - 1) >> blk_sh);
                     if (dead) {
                         nb = L2F_DEAD;
-                    } else if (need == 1 && spare != L2F_NONE) {
-                        nb = spare;   // reserved a tile or more ago: no wait
-                        spare = L2F_NONE;
-                        nlim = reg_base[gb + d + 1];
-                        nneed = 1;
                     } else if (need) {
                         nb = atomicAdd(&reg_cur[gb + d], (unsigned long long)need * BLK);
                         nlim = reg_base[gb + d + 1];
@@ -1786,13 +1767,6 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
                 }
                 nbase[d] = nb;
 #endif
-                // the next spare: once this tile leaves fewer than
-                // L2F_SPARE_LOW free slots in the region's current block
-                // (not on the last tile; never for an overflowed region)
-                const uint32_t e1 = c0 + h;
-                const uint32_t free_after = (BLK - (e1 & (BLK - 1))) & (BLK - 1);
-                if (!last && !dead && nb != L2F_DEAD && spare == L2F_NONE && e1 > 0 && free_after < L2F_SPARE_LOW)
-                    spare = atomicAdd(&reg_cur[gb + d], (unsigned long long)BLK);
                 const uint32_t a = c0 & ~(SEG - 1), e = c0 + h;
                 fl = !dead && c0 != a && (last ? e : (e & ~(SEG - 1))) > a;
             }
@@ -1804,9 +1778,6 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
                 if (fl) flist[base + (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63)) - 1))] = (uint16_t)d;
             }
         }
-        // the next tile's records: after the reservations, so the wait for a
-        // spare (next tile) never includes these loads
-        load_tile(t0 + TILE, v);
         PH(2);
         block_sync();
         PH(3);
@@ -1861,23 +1832,13 @@ __global__ void __launch_bounds__(THREADS) k_scatter_l2f(uint32_t nbk, int s0, i
         }
     }
     PH_END(32, 8);
-    // the rest of every partially filled block: sentinels; an unused spare
-    // (a whole block, past the region's capacity when it overflowed): sentinels
+    // the rest of every partially filled block: sentinels
     block_sync();
     for (uint32_t y = threadIdx.x; y < F2 * BLK; y += THREADS) {
         const uint32_t d = y >> blk_sh, sl = y & (BLK - 1);
         const uint32_t c = cnt[d] & (BLK - 1);
         if (c == 0 || sl < c || bcur[d] == L2F_DEAD) continue;
         rec_out[bcur[d] + sl] = ~0ull;
-    }
-    if (threadIdx.x < F2 && spare != L2F_NONE) {
-        const uint32_t d = threadIdx.x;
-        if (spare + BLK <= reg_base[gb + d + 1]) {
-            for (uint32_t sl = 0; sl < BLK; sl += 2)
-                *(ulonglong2 *)(rec_out + spare + sl) = make_ulonglong2(~0ull, ~0ull);
-        } else {
-            atomicOr((unsigned long long *)&ctr[CTR_ERR], 4ull);
-        }
     }
 }
 
