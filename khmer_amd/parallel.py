@@ -182,6 +182,24 @@ class HostTransport(object):
         self.error = None
         world = rdv.world
 
+        import time as _time
+        beat = {"t": _time.time(), "n": 0}
+
+        def _beat(fn):
+            """A progress line on rank 0's stderr at most every 20 s: a long
+            host-transport consume (the bench's multi-rank dry run moves GBs
+            per pass through the rendezvous) keeps writing."""
+            def call(*a):
+                rc = fn(*a)
+                beat["n"] += 1
+                if rdv.rank == 0 and _time.time() - beat["t"] > 20:
+                    import sys
+                    beat["t"] = _time.time()
+                    sys.stderr.write("host transport: %d collectives done\n" % beat["n"])
+                    sys.stderr.flush()
+                return rc
+            return call
+
         def failed(e):
             import sys
             self.error = e
@@ -231,7 +249,7 @@ class HostTransport(object):
             except Exception as e:
                 return failed(e)
 
-        self._fns = (_AG(allgather), _BC(broadcast), _A2A(alltoallv))
+        self._fns = (_AG(_beat(allgather)), _BC(_beat(broadcast)), _A2A(_beat(alltoallv)))
         self.struct = _KhTransport(None, *self._fns)
 
 
