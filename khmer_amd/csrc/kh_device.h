@@ -49,6 +49,27 @@ KH_HD uint64_t mod_barrett(uint64_t h, uint64_t p, uint64_t m) {
     return r >= p ? r - p : r;
 }
 
+// The same remainder from one double multiply, for p < 2^30 and h / p < 2^31
+// (Params::fm32; fewer VALU instructions than the 64-bit Barrett product):
+// with ip = fl(1/p), x = fl(fl(h) * ip) is within 2^-20 of h / p, so q =
+// trunc(x) is floor(h / p) or one off, the remainder estimate h - q * p lies
+// in [-p, 2p) -- exact in 32-bit two's complement -- and one correction each
+// way makes it h % p.
+KH_HD uint32_t mod_f64_32(uint64_t h, uint32_t p, double ip) {
+    const uint32_t q = (uint32_t)((double)h * ip);
+    int32_t r = (int32_t)((uint32_t)h - q * p);
+    r += r < 0 ? (int32_t)p : 0;
+    r -= r >= (int32_t)p ? (int32_t)p : 0;
+    return (uint32_t)r;
+}
+// floor(x / d) for x < 2^53 and a quotient below 2^31 (SrcCommon::kpr_ip),
+// the same bound: the double estimate is exact or one off either way
+KH_HD uint64_t div_f64(uint64_t x, uint64_t d, double id) {
+    const uint32_t q = (uint32_t)((double)x * id);
+    const int64_t r = (int64_t)(x - (uint64_t)q * d);
+    return r < 0 ? q - 1 : (r >= (int64_t)d ? q + 1 : q);
+}
+
 KH_HD uint64_t kmer_mask(int k) { return k >= 32 ? ~0ull : ((1ull << (2 * k)) - 1); }
 
 KH_HD uint64_t bitrev64(uint64_t x) {

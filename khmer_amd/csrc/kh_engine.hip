@@ -1295,9 +1295,12 @@ static void run_pass(Graph *g, const Src &src, uint64_t nkmers, const PassOut *o
 
 // ---------------------------------------------------------------------------
 // batching of read sets
-static void set_fixed(SrcCommon &s, uint64_t kpr) {
+// fixed-length reads of kpr k-mers; nreads bounds the read index of the
+// buffer the source walks (div_f64 needs it below 2^31)
+static void set_fixed(SrcCommon &s, uint64_t kpr, uint64_t nreads) {
     s.kpr = kpr;
     s.kpr_m = kpr ? barrett_m(kpr) : 0;
+    s.kpr_ip = kpr && nreads < (1ull << 31) && nreads * kpr < (1ull << 52) ? 1.0 / (double)kpr : 0.0;
 }
 
 template <class Src>
@@ -1305,7 +1308,7 @@ static void consume_reads(Graph *g, Src base, const uint64_t *d_koff, uint64_t n
                           uint64_t kpr, const PassOut *out) {
     if (nkmers == 0 || nreads == 0) return;
     const uint64_t B = g->batch_kmers;
-    set_fixed(base, kpr);
+    set_fixed(base, kpr, nreads);
     base.koff = d_koff;
     base.nreads = nreads;
     base.kbase = 0;
@@ -1650,7 +1653,7 @@ void engine_median_fixed_device(Graph *g, const void *d_reads, uint64_t nreads, 
             const uint64_t n = std::min(cr, nreads - r0);
             const uint8_t *rd = padded_bytes(g, (const uint8_t *)d_reads + r0 * read_len, n * read_len);
             SrcBytes s = src_bytes(g, rd, nullptr, n, kpr, n * read_len);
-            set_fixed(s, kpr);
+            set_fixed(s, kpr, n);
             const unsigned gr = (unsigned)std::min<uint64_t>((n + 3) / 4, 8192);
             TIMED("median", hipLaunchKernelGGL(k_median_fixed<SrcBytes>, dim3(gr), dim3(256), 0, g->stream, g->prm,
                                                s, n, (uint32_t)kpr, g->d_tab, g->d_bc_keys, g->d_bc_vals, g->d_bc_n,
@@ -1658,7 +1661,7 @@ void engine_median_fixed_device(Graph *g, const void *d_reads, uint64_t nreads, 
         }
     } else {
         SrcTwoBit s = src_twobit(g, (const uint64_t *)d_reads);
-        set_fixed(s, kpr);
+        set_fixed(s, kpr, nreads);
         TIMED("median", hipLaunchKernelGGL(k_median_fixed<SrcTwoBit>, dim3(grid), dim3(256), 0, g->stream, g->prm, s,
                                            nreads, (uint32_t)kpr, g->d_tab, g->d_bc_keys, g->d_bc_vals, g->d_bc_n,
                                            d_med, d_avg, d_sd));
@@ -1759,6 +1762,7 @@ void graph_prepare_params(Graph *g) {
     for (int i = 0; i < g->n; i++) {
         P.p[i] = g->sizes[i];
         P.m[i] = barrett_m(g->sizes[i]);
+        P.ip[i] = 1.0 / (double)g->sizes[i];
         P.lo[i] = g->lo[i];
         P.lsz[i] = g->lsz[i];
         P.tbase[i] = base;
@@ -1767,6 +1771,13 @@ void graph_prepare_params(Graph *g) {
         P.tbytes[i] = g->nbytes[i];
         byteoff += (g->nbytes[i] + 255) / 256 * 256;
     }
+    // local_bin's double-multiply remainder: every table below 2^30 bins and
+    // every hash below 2^31 table sizes (2-bit k-mers are below 4^k; Murmur
+    // hashes span 64 bits)
+    const double hmax = g->hash == TWOBIT && g->k < 32 ? std::ldexp(1.0, 2 * g->k) : std::ldexp(1.0, 64);
+    P.fm32 = 1;
+    for (int i = 0; i < g->n; i++)
+        if (g->sizes[i] >= (1ull << 30) || hmax >= std::ldexp((double)g->sizes[i], 31)) P.fm32 = 0;
     uint64_t F1 = base / span;
     if (F1 > 4096) fail(KH_EVALUE, "tables too large for one device (more than 4096 level-1 buckets)");
     if (F1 == 0) F1 = 1;
@@ -2828,7 +2839,7 @@ static Src group_src(Graph *g, const GroupReads &R, const void *buf, uint64_t r0
 template <>
 SrcTwoBit group_src<SrcTwoBit>(Graph *g, const GroupReads &R, const void *buf, uint64_t r0, uint64_t nr) {
     SrcTwoBit s = src_twobit(g, (const uint64_t *)buf);
-    set_fixed(s, R.kpr);
+    set_fixed(s, R.kpr, R.nreads);
     s.koff = nullptr;
     s.nreads = nr;
     s.kbase = r0 * R.kpr;
@@ -2841,7 +2852,7 @@ SrcBytes group_src<SrcBytes>(Graph *g, const GroupReads &R, const void *buf, uin
     // the pass's reverse-complement stream goes to g's workspace
     const uint8_t *b = padded_bytes(g, (const uint8_t *)buf + r0 * R.read_len, nr * R.read_len);
     SrcBytes s = src_bytes(g, b, nullptr, nr, R.kpr, nr * R.read_len);
-    set_fixed(s, R.kpr);
+    set_fixed(s, R.kpr, R.nreads);
     s.koff = nullptr;
     s.nreads = nr;
     s.kbase = 0;

@@ -104,6 +104,8 @@ struct Params {
     uint64_t lo[MAXT];        // first bin of table i held here (0 unless sharded)
     uint64_t lsz[MAXT];       // bins of table i held here (p[i] unless sharded)
     uint64_t m[MAXT];         // Barrett constants
+    double ip[MAXT];          // 1 / p[i] (mod_f64_32) when fm32
+    int fm32;                 // every p[i] < 2^30 and every hash / p[i] < 2^31: local_bin uses mod_f64_32
     uint64_t tbase[MAXT];     // global bin base of table i
     uint64_t tbyte[MAXT];     // byte offset of table i in the table arena
     uint64_t tbytes[MAXT];    // storage bytes of table i

@@ -544,7 +544,7 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
     // first word of tile [j0, ..) (TW)
     auto tile_w0 = [&](uint64_t j0) -> uint64_t {
         const uint64_t ja = j0 + src.kbase;
-        return ((ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2) >> 6;
+        return ((ja + src.read_of(ja) * (uint64_t)(src.k - 1)) * 2) >> 6;
     };
     // words [tile_w0(j0), tile_w0(j1 - 1) + 1] hold every window of tile [j0, j1)
     auto tile_nw = [&](uint64_t j0, uint64_t j1) -> uint32_t { return (uint32_t)(tile_w0(j1 - 1) + 2 - tile_w0(j0)); };
@@ -593,7 +593,7 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
                 uint64_t h = 0;
                 if (j < j1) {
                     const uint64_t ja = j + src.kbase;
-                    const uint64_t bpos = (ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2;
+                    const uint64_t bpos = (ja + src.read_of(ja) * (uint64_t)(src.k - 1)) * 2;
                     const uint32_t wi = (uint32_t)((bpos >> 6) - tw_w0);
                     h = src.finish(SrcTwoBit::Pend{tw_cur[wi], tw_cur[wi + 1], (uint32_t)(bpos & 63)});
                 }
@@ -881,7 +881,7 @@ __global__ void __launch_bounds__(L1_THREADS, L1F_WAVES_PER_EU) k_scatter_l1p(Pa
     bool htop = true;                                         // the hashed tile starts a chunk
     auto tile_w0 = [&](uint64_t j0) -> uint64_t {
         const uint64_t ja = j0 + src.kbase;
-        return ((ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2) >> 6;
+        return ((ja + src.read_of(ja) * (uint64_t)(src.k - 1)) * 2) >> 6;
     };
     auto tile_nw = [&](uint64_t j0, uint64_t j1) -> uint32_t { return (uint32_t)(tile_w0(j1 - 1) + 2 - tile_w0(j0)); };
     // the tile after the hashed one: [*n0, *n1), empty when there is none
@@ -912,7 +912,7 @@ __global__ void __launch_bounds__(L1_THREADS, L1F_WAVES_PER_EU) k_scatter_l1p(Pa
             uint64_t x = 0;
             if (j < j1) {
                 const uint64_t ja = j + src.kbase;
-                const uint64_t bpos = (ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2;
+                const uint64_t bpos = (ja + src.read_of(ja) * (uint64_t)(src.k - 1)) * 2;
                 const uint32_t wi = (uint32_t)((bpos >> 6) - tw_w0);
                 x = src.finish(SrcTwoBit::Pend{tw_cur[wi], tw_cur[wi + 1], (uint32_t)(bpos & 63)});
             }
@@ -1285,7 +1285,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
     }
     auto tile_w0 = [&](uint64_t j0) -> uint64_t {
         const uint64_t ja = j0 + src.kbase;
-        return ((ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2) >> 6;
+        return ((ja + src.read_of(ja) * (uint64_t)(src.k - 1)) * 2) >> 6;
     };
     auto tile_nw = [&](uint64_t j0, uint64_t j1) -> uint32_t { return (uint32_t)(tile_w0(j1 - 1) + 2 - tile_w0(j0)); };
     uint64_t tw_next = 0;
@@ -1406,7 +1406,7 @@ __global__ void __launch_bounds__(L1_THREADS) k_own_l1f(Params P, Src src, uint6
                 uint64_t h = 0;
                 if (j < j1) {
                     const uint64_t ja = j + src.kbase;
-                    const uint64_t bpos = (ja + div_barrett(ja, src.kpr, src.kpr_m) * (uint64_t)(src.k - 1)) * 2;
+                    const uint64_t bpos = (ja + src.read_of(ja) * (uint64_t)(src.k - 1)) * 2;
                     const uint32_t wi = (uint32_t)((bpos >> 6) - tw_w0);
                     h = src.finish(SrcTwoBit::Pend{tw_cur[wi], tw_cur[wi + 1], (uint32_t)(bpos & 63)});
                 }

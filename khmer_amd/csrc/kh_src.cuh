@@ -32,7 +32,12 @@ struct SrcCommon {
     uint64_t kbase;         // absolute index of batch k-mer 0
     uint64_t rbase;         // absolute index of koff[0]'s read
     uint64_t kpr, kpr_m;    // fixed k-mers per read and its Barrett constant (0 = variable)
+    double kpr_ip = 0;      // 1 / kpr when every read index is below 2^31 (div_f64), else 0
     int k;
+    // read of absolute k-mer index ja (fixed-length reads)
+    __device__ __forceinline__ uint64_t read_of(uint64_t ja) const {
+        return kpr_ip != 0.0 ? div_f64(ja, kpr, kpr_ip) : div_barrett(ja, kpr, kpr_m);
+    }
 };
 
 // Every source also splits a hash into fetch() (issue the global loads) and
@@ -140,7 +145,7 @@ __device__ __forceinline__ uint64_t kmer_hash(const Src &src, const uint64_t *s_
     } else {
         uint64_t r;
         if (src.kpr) {
-            r = div_barrett(ja, src.kpr, src.kpr_m);
+            r = src.read_of(ja);
         } else {
             uint32_t lo = 0, hi = tr.n;
             while (hi - lo > 1) {
@@ -159,7 +164,7 @@ template <class Src>
 __device__ __forceinline__ typename Src::Pend kmer_fetch(const Src &src, uint64_t j) {
     const uint64_t ja = j + src.kbase;
     if constexpr (!Src::kReads) return src.fetch(ja, 0);
-    else return src.fetch(ja, div_barrett(ja, src.kpr, src.kpr_m));
+    else return src.fetch(ja, src.read_of(ja));
 }
 
 // hash of batch k-mer j without a tile window (rare paths: bigcount, outputs)
@@ -171,7 +176,7 @@ __device__ __forceinline__ uint64_t kmer_hash_global(const Src &src, uint64_t j)
     } else {
         uint64_t r;
         if (src.kpr) {
-            r = div_barrett(ja, src.kpr, src.kpr_m);
+            r = src.read_of(ja);
         } else {
             uint64_t lo = 0, hi = src.nreads;
             while (hi - lo > 1) {
@@ -187,7 +192,7 @@ __device__ __forceinline__ uint64_t kmer_hash_global(const Src &src, uint64_t j)
 // bin of hash h in table i (h mod p_i, storage.hh:577) as a bin of the local
 // bin space (table bases P.tbase); false when another shard owns it
 __device__ __forceinline__ bool local_bin(const Params &P, int i, uint64_t h, uint64_t *G) {
-    const uint64_t b = mod_barrett(h, P.p[i], P.m[i]) - P.lo[i];
+    const uint64_t b = (P.fm32 ? (uint64_t)mod_f64_32(h, (uint32_t)P.p[i], P.ip[i]) : mod_barrett(h, P.p[i], P.m[i])) - P.lo[i];
     *G = P.tbase[i] + b;
     return b < P.lsz[i];
 }
