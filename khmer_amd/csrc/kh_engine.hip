@@ -639,7 +639,7 @@ static void move_kstats(Graph *dst, Graph *src) {
 
 // level-1 scatter instance for a tail mode and k-mers per thread (8 / nt)
 template <class Src>
-using L1Fn = void (*)(Params, Src, uint64_t, uint32_t, uint32_t, int, int, uint64_t *, uint64_t *, uint32_t);
+using L1Fn = void (*)(Params, Src, uint64_t, uint32_t, uint32_t, int, int, uint64_t *, uint64_t *, uint32_t, uint32_t);
 template <class Src>
 static L1Fn<Src> l1_kernel(bool seg, int kpt) {
     switch (kpt) {
@@ -1105,7 +1105,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
             TIMED("scatter_l1", hipLaunchKernelGGL((k_scatter_l1<SrcHashes, 2, L1_MAX_RPT, L1_MAX_RPT, true>),
                                                    dim3(nch), dim3(L1_THREADS),
                                                    lds_scatter_l1(P, false, L1_THREADS * L1_MAX_RPT), st, P, rs, nrec,
-                                                   (uint32_t)L2_CHUNK, nch, 0, 1, w.moff, w.rec1, 0u));
+                                                   (uint32_t)L2_CHUNK, nch, 0, 1, w.moff, w.rec1, 0u, 0u));
         } else {
             TIMED("hist_l1", hipLaunchKernelGGL(k_hist_l1<Src>, dim3(q.nch1), dim3(L1_THREADS), lds_hist_l1(P, window),
                                                 st, P, src, nkmers, q.ck1, q.nch1, w.mcnt));
@@ -1119,13 +1119,36 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
                 KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
                 KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
             }
-            for (int t0 = 0; t0 < P.n; t0 += L1_MAX_RPT) {
-                const int nt = std::min(L1_MAX_RPT, P.n - t0);
+            // Table groups of up to 8 per launch.  Above 1024 buckets (C4, C5:
+            // 1908), each launch takes the tables whose buckets fit 1024 and
+            // holds only those in LDS: the 2-record tails then fit beside the
+            // tile at two workgroups a CU, for one more hash of each k-mer
+            // (measured C4 570.1 -> 563.5, C5 516.7 -> 505.9 ms/step,
+            // profiles/r5/ab_l1_exact_windows.txt).  KH_L1X_NT fixes the
+            // tables per launch (development A/B).
+            static const int xnt = env_seg("KH_L1X_NT", 0);
+            const int shift = P.s0 + P.s2;
+            auto bstart = [&](int i) { return i < P.n ? (uint32_t)(P.tbase[i] >> shift) : P.F1; };
+            for (int t0 = 0, nt = 0; t0 < P.n; t0 += nt) {
+                if (xnt > 0) {
+                    nt = std::min({xnt, L1_MAX_RPT, P.n - t0});
+                } else if (P.F1 <= 1024) {
+                    nt = std::min(L1_MAX_RPT, P.n - t0);
+                } else {
+                    nt = 1;
+                    while (t0 + nt < P.n && nt < L1_MAX_RPT && bstart(t0 + nt + 1) - bstart(t0) <= 1024) nt++;
+                }
                 const int kpt = std::max(1, L1_MAX_RPT / nt);
                 const int tile_kmers = L1_THREADS * kpt;
-                TIMED("scatter_l1", hipLaunchKernelGGL(l1_kernel<Src>(l1_seg(P) != 0, kpt), dim3(q.nch1),
-                                                       dim3(L1_THREADS), lds_scatter_l1(P, window, tile_kmers), st, P,
-                                                       src, nkmers, q.ck1, q.nch1, t0, nt, w.moff, w.rec1, 0u));
+                Params Q = P;
+                uint32_t bb0 = 0;
+                if (nt < P.n) {   // window: the buckets of tables [t0, t0 + nt)
+                    bb0 = bstart(t0);
+                    Q = win_params(P, L1Win{t0, nt, bb0, bstart(t0 + nt) - bb0});
+                }
+                TIMED("scatter_l1", hipLaunchKernelGGL(l1_kernel<Src>(l1_seg(Q) != 0, kpt), dim3(q.nch1),
+                                                       dim3(L1_THREADS), lds_scatter_l1(Q, window, tile_kmers), st, Q,
+                                                       src, nkmers, q.ck1, q.nch1, t0, nt, w.moff, w.rec1, 0u, bb0));
             }
         }
         if (check_mode() && !l1f && !ownf) check_holes(g, w.rec1, nrec, "scatter_l1");
@@ -2486,7 +2509,7 @@ static void a2a_level1(Graph *V, const Src &src, uint64_t nkmers, uint32_t jbase
             TIMED_G(V, "scatter_l1", hipLaunchKernelGGL(l1_kernel<Src>(l1_seg(P) != 0, kpt), dim3(q.nch1),
                                                         dim3(L1_THREADS), lds_scatter_l1(P, false, L1_THREADS * kpt),
                                                         st, P, src, nkmers, q.ck1, q.nch1, t0, nt, w.moff, w.rec1,
-                                                        jbase));
+                                                        jbase, 0u));
         }
         KH_HIP(hipGetLastError());
         return;

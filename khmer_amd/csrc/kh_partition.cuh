@@ -312,7 +312,7 @@ __global__ void __launch_bounds__(1024) k_plan_l2(uint32_t F1, uint32_t nch1, co
 template <class Src, int SEG, int KPT, int RPT = L1_MAX_RPT, bool PRE = false>
 __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, uint64_t nkmers, uint32_t ck1,
                                                           uint32_t nch1, int t0, int nt, uint64_t *O1,
-                                                          uint64_t *rec, uint32_t jbase) {
+                                                          uint64_t *rec, uint32_t jbase, uint32_t bb0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t F1 = P.F1;
     const uint32_t F1a = (F1 + 3) & ~3u;
@@ -332,6 +332,9 @@ __global__ void __launch_bounds__(L1_THREADS) k_scatter_l1(Params P, Src src, ui
     const uint64_t omask = (1ull << shift) - 1;
     constexpr int TILE_KMERS = L1_THREADS * KPT;
 
+    // a launch window of buckets [bb0, bb0 + F1) (P's geometry shifted to it):
+    // rows bb0 + b of the count matrix
+    O1 += (uint64_t)bb0 * nch1;
     for (uint32_t b = threadIdx.x; b < F1; b += blockDim.x) em.init(b, O1[(uint64_t)b * nch1 + blockIdx.x]);
     const uint64_t c0 = (uint64_t)blockIdx.x * ck1;
     const uint64_t c1 = min(nkmers, c0 + ck1);

@@ -60,9 +60,10 @@ def main():
         wr.writerows(rows)
     dom = bench["roofline"]["kernel"]
     per = {timer_name(r["kernel"]): r["hbm_bytes_per_launch"] for r in rows}
-    # the bench's roofline.traffic source: the default (C2 consume) workload
-    # only; other profiles (e.g. <tag>_query) keep their csv alone
-    traffic_json = os.path.join(prof, "pmc_traffic.json" if not tag.endswith("_query") else "%s_traffic.json" % tag)
+    # the bench's roofline.traffic source: the headline (C2 consume) workload
+    # only; other profiles (C4, C5, queries) go to <tag>_traffic.json
+    headline = bench["config"]["workload"].startswith("Countgraph k=21 4x1e+09, consume of 50000000 ")
+    traffic_json = os.path.join(prof, "pmc_traffic.json" if headline else "%s_traffic.json" % tag)
     json.dump({"kernel": dom, "config": bench["config"]["workload"],
                "hbm_bytes_per_launch": per.get(dom),
                "kernels": per,
@@ -83,7 +84,7 @@ def timer_name(device_kernel):
     if base == "apply_bit":
         return "apply_bit"
     # the fixed-capacity partitions time under the same names as the exact ones
-    return {"scatter_l1f": "scatter_l1", "scatter_l2f": "scatter_l2", "hist_wf": "hist_w", "scatter_wf": "scatter_w",
+    return {"scatter_l1f": "scatter_l1", "scatter_l1p": "scatter_l1", "scatter_l2f": "scatter_l2", "hist_wf": "hist_w", "scatter_wf": "scatter_w",
             "mark_wf": "mark", "median_fixed": "median"}.get(base, base)
 
 
