@@ -177,10 +177,13 @@ __device__ __forceinline__ uint64_t winner_base(const uint32_t *s_wt, uint32_t *
 }
 
 // Byte (KIND == BYTE) and Nibble storage: ByteStorage::add / NibbleStorage::add
-// (storage.hh:571-624 / 320-359) applied as a batch
+// (storage.hh:571-624 / 320-359) applied as a batch.  LOS: complement mode of
+// the coarse-window runs -- they carry the pass's losers (every record that is
+// not its bin's is_new first insert) instead of its winners, for passes where
+// most inserts are winners (sparse tables); k_mark_wf counts them per k-mer.
 // TH threads, 16 bins per thread: regions of 2^13 (512 threads) or 2^14 bins
 // (1024 threads) -- one kernel body for both
-template <int KIND, int TH>
+template <int KIND, int TH, bool LOS = false>
 __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int BPT = 16;               // bins per thread: R == 16 * TH
@@ -278,6 +281,7 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
             if (t == 0) s_flag[0] = s_flag[1] = 0;
         }
         if (t < MAX_CW) chist[t] = ccur[t] = 0;
+        if (LOS && t == 0) s_flag[2] = 0;   // losers listed
         PH(5);
         block_sync();
         PH(0);
@@ -413,7 +417,45 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
             // barrier; wave 0's returning reservation atomics complete
             // meanwhile; consecutive lanes write the runs.
             const int cjs = A.cjs;
-            if (nw) {
+            if constexpr (LOS) {
+                // complement mode: the region's records again (L2-resident:
+                // the count loop just read them), each a loser unless its bin
+                // was zero before the pass and its k-mer index is the bin's
+                // minimum; losers are counted per coarse window and listed
+                // unsorted in the dead count array (a region's records fit its
+                // 2^s0 entries: the host's reg_max check)
+                block_sync();   // pass 1's wflag / minj of every bin
+                const uint32_t lane = t & 63;
+                const uint64_t pend = (ri.e1 + 1) >> 1;
+                for (uint64_t pr0 = ri.e0 >> 1; pr0 < pend; pr0 += TH) {   // uniform trip count (ballots)
+                    const uint64_t pr = pr0 + t, r = 2 * pr;
+                    uint64_t xs[2] = {~0ull, ~0ull};
+                    if (pr < pend) {
+                        const ulonglong2 xx = *(const ulonglong2 *)(A.rec + r);
+                        if (r >= ri.e0) xs[0] = xx.x;
+                        if (r + 1 < ri.e1) xs[1] = xx.y;
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint64_t x = xs[h];
+                        bool lose = false;
+                        const uint32_t j = (uint32_t)(x >> 32);
+                        if (x != ~0ull) {
+                            const uint32_t o = (uint32_t)x;
+                            lose = !(((wflag[o >> 2] >> (o & 3)) & 1u) && minj[o] == j);
+                        }
+                        const uint64_t m = __ballot(lose);
+                        if (!m) continue;
+                        uint32_t base = 0;
+                        if (lane == 0) base = atomicAdd(&s_flag[2], (uint32_t)__popcll(m));
+                        base = __shfl(base, 0, 64);
+                        if (lose) {
+                            cnt[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = j;
+                            atomicAdd(&chist[j >> cjs], 1u);
+                        }
+                    }
+                }
+            } else if (nw) {
 #pragma unroll
                 for (int step = 0; step < BPT / 4; step++) {
                     const uint32_t g = t + (uint32_t)step * TH;
@@ -450,19 +492,32 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
             if (t < 64 && cc && !(KH_ABL(P, 512))) my_gb = atomicAdd(&A.cw_cur[t], (unsigned long long)cc);   // 512: timing only
             PH(7);
             uint32_t *wst = cnt;
+            if constexpr (LOS) {
+                // the listed losers, counting-sorted by window into the dead
+                // min-j array (window starts through LDS, one more barrier)
+                if (t < 64) cst0[t] = st0;
+                block_sync();
+                wst = minj;
+                const uint32_t nl = s_flag[2];
+                for (uint32_t x = t; x < nl; x += TH) {
+                    const uint32_t j = cnt[x], c = j >> cjs;
+                    wst[cst0[c] + atomicAdd(&ccur[c], 1u)] = j;
+                }
+            } else {
 #pragma unroll
-            for (int step = 0; step < BPT / 4; step++) {
-                const uint32_t g = t + (uint32_t)step * TH;
-                const uint32_t win = wflag[g];
-                if (!__ballot(win != 0)) continue;   // wave-uniform: the shuffles below need every lane
-                const uint4 m = ((const uint4 *)minj)[g];
-                const uint32_t mv[4] = {m.x, m.y, m.z, m.w};
+                for (int step = 0; step < BPT / 4; step++) {
+                    const uint32_t g = t + (uint32_t)step * TH;
+                    const uint32_t win = wflag[g];
+                    if (!__ballot(win != 0)) continue;   // wave-uniform: the shuffles below need every lane
+                    const uint4 m = ((const uint4 *)minj)[g];
+                    const uint32_t mv[4] = {m.x, m.y, m.z, m.w};
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const bool ok = (win >> k) & 1u;
-                    const uint32_t c = ok ? mv[k] >> cjs : 0u;
-                    const uint32_t base = __shfl(st0, (int)c, 64);
-                    if (ok) wst[base + atomicAdd(&ccur[c], 1u)] = mv[k];
+                    for (int k = 0; k < 4; k++) {
+                        const bool ok = (win >> k) & 1u;
+                        const uint32_t c = ok ? mv[k] >> cjs : 0u;
+                        const uint32_t base = __shfl(st0, (int)c, 64);
+                        if (ok) wst[base + atomicAdd(&ccur[c], 1u)] = mv[k];
+                    }
                 }
             }
             if (t == 0) A.wcnt[rr] = wall;
@@ -834,12 +889,13 @@ constexpr int WF_THREADS = 1024;
 constexpr int WF_RPT = 8;
 constexpr int WF_TILE = WF_THREADS * WF_RPT;
 constexpr uint32_t WF_CHUNK = 16 * WF_TILE;   // winners per chunk
+constexpr uint32_t FPC_MAX = 256;             // fine windows per coarse window (complement mode: 256)
 
 __global__ void __launch_bounds__(WF_THREADS) k_hist_wf(const uint32_t *wco, const WChunk *chunks, int js,
                                                         uint32_t fpc, uint32_t *M) {
-    __shared__ uint32_t hist[MAX_CW];
+    __shared__ uint32_t hist[FPC_MAX];
     const WChunk ch = chunks[blockIdx.x];
-    if (threadIdx.x < MAX_CW) hist[threadIdx.x] = 0;
+    if (threadIdx.x < FPC_MAX) hist[threadIdx.x] = 0;
     block_sync();
     // eight loads in flight per thread
     for (uint64_t i0 = ch.start; i0 < ch.end; i0 += 8 * WF_THREADS) {
@@ -860,8 +916,8 @@ __global__ void __launch_bounds__(WF_THREADS) k_hist_wf(const uint32_t *wco, con
 __global__ void __launch_bounds__(WF_THREADS) k_scatter_wf(const uint32_t *wco, const WChunk *chunks, int js,
                                                            uint32_t fpc, const uint64_t *O, uint32_t *wout) {
     __shared__ uint32_t stage[WF_TILE];
-    __shared__ uint32_t hist[MAX_CW], lstart[MAX_CW];
-    __shared__ uint64_t cur[MAX_CW];
+    __shared__ uint32_t hist[FPC_MAX], lstart[FPC_MAX];
+    __shared__ uint64_t cur[FPC_MAX];
     const WChunk ch = chunks[blockIdx.x];
     if (threadIdx.x < fpc) {
         cur[threadIdx.x] = O[ch.mbase + (uint64_t)threadIdx.x * ch.nk + ch.k];
@@ -879,14 +935,25 @@ __global__ void __launch_bounds__(WF_THREADS) k_scatter_wf(const uint32_t *wco, 
             if (v[q] != NO_J) rank[q] = atomicAdd(&hist[(v[q] >> js) & (fpc - 1)], 1u);
         }
         block_sync();
-        if (threadIdx.x < 64) {
-            const uint32_t c = threadIdx.x < fpc ? hist[threadIdx.x] : 0;
-            uint32_t incl = c;
+        if (threadIdx.x < 64) {   // lane l: fine windows 4l .. 4l + 3
+            const uint32_t l = threadIdx.x;
+            uint32_t c4[4], sum = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                c4[k] = 4 * l + k < fpc ? hist[4 * l + k] : 0;
+                sum += c4[k];
+            }
+            uint32_t incl = sum;
             for (int d = 1; d < 64; d <<= 1) {
                 const uint32_t y = __shfl_up(incl, d, 64);
-                if (threadIdx.x >= (uint32_t)d) incl += y;
+                if (l >= (uint32_t)d) incl += y;
             }
-            if (threadIdx.x < fpc) lstart[threadIdx.x] = incl - c;
+            uint32_t acc = incl - sum;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (4 * l + k < fpc) lstart[4 * l + k] = acc;
+                acc += c4[k];
+            }
         }
         block_sync();
 #pragma unroll
@@ -907,12 +974,18 @@ __global__ void __launch_bounds__(WF_THREADS) k_scatter_wf(const uint32_t *wco, 
 }
 
 // one workgroup per fine window: its winners' LDS bitmap -> n_unique (and the
-// per-k-mer new flags when asked); range [O[mbase(c) + f*nk_c], next)
+// per-k-mer new flags when asked); range [O[mbase(c) + f*nk_c], next).
+// Complement mode (ntab != 0): the range holds losers, one per (k-mer, table)
+// the k-mer did not win; a k-mer is new unless it lost in all ntab tables
+// (ByteStorage::add's is_new, storage.hh:571-588), so the window counts losers
+// per k-mer in 4-bit LDS counters (ntab <= 15) and its k-mers [0, nkmers) with
+// a count below ntab are the new ones.
 __global__ void __launch_bounds__(PT_THREADS) k_mark_wf(const uint32_t *wout, const uint64_t *O,
                                                         const uint64_t *cmbase, const uint32_t *cnk, uint32_t fpc,
-                                                        int js, uint64_t *ctr, uint32_t *newbits) {
+                                                        int js, uint64_t *ctr, uint32_t *newbits, uint32_t ntab,
+                                                        uint64_t nkmers) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t *bits = (uint32_t *)smem;   // [2^js / 32]
+    uint32_t *bits = (uint32_t *)smem;   // [2^js / 32] (complement mode: [2^js / 8] 4-bit counts)
     const uint32_t nw = 1u << (js - 5);
     const uint32_t fw = blockIdx.x, c = fw / fpc, f = fw % fpc;
     const uint32_t nk = cnk[c];
@@ -920,6 +993,47 @@ __global__ void __launch_bounds__(PT_THREADS) k_mark_wf(const uint32_t *wout, co
     if (nk) {   // O has one entry past the matrix (the total): (c, f + 1)'s start ends (c, f)
         s = O[cmbase[c] + (uint64_t)f * nk];
         e = O[cmbase[c] + (uint64_t)(f + 1) * nk];
+    }
+    if (ntab) {
+        const uint32_t ncw = 1u << (js - 3);   // count words
+        for (uint32_t t = threadIdx.x; t < ncw / 4; t += blockDim.x) ((uint4 *)bits)[t] = make_uint4(0, 0, 0, 0);
+        block_sync();
+        const uint32_t mask = (1u << js) - 1;
+        for (uint64_t q0 = s; q0 < e; q0 += 8 * (uint64_t)blockDim.x) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint64_t q = q0 + (uint64_t)u * blockDim.x + threadIdx.x;
+                v[u] = q < e ? wout[q] : NO_J;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (v[u] != NO_J) {
+                    const uint32_t j = v[u] & mask;
+                    atomicAdd(&bits[j >> 3], 1u << (4 * (j & 7)));
+                }
+        }
+        block_sync();
+        const uint64_t j0 = (uint64_t)fw << js;
+        const uint32_t nvalid = (uint32_t)min((uint64_t)1 << js, nkmers - j0);
+        uint64_t uniq = 0;
+        for (uint32_t t = threadIdx.x; t < nw; t += blockDim.x) {   // 32 k-mers: four count words
+            const uint4 x = ((const uint4 *)bits)[t];
+            const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+            uint32_t nb = 0;
+#pragma unroll
+            for (int w4 = 0; w4 < 4; w4++)
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t jl = 32 * t + 8 * w4 + k;
+                    if (jl < nvalid && ((xw[w4] >> (4 * k)) & 15u) != ntab) nb |= 1u << (8 * w4 + k);
+                }
+            uniq += __popc(nb);
+            if (newbits) newbits[(uint64_t)fw * nw + t] = nb;
+        }
+        uniq = wave_sum(uniq);
+        if ((threadIdx.x & 63) == 0 && uniq) atomicAdd((unsigned long long *)&ctr[CTR_UNIQUE], (unsigned long long)uniq);
+        return;
     }
     for (uint32_t t = threadIdx.x; t < nw / 4; t += blockDim.x) ((uint4 *)bits)[t] = make_uint4(0, 0, 0, 0);
     block_sync();

@@ -232,7 +232,7 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
     const uint64_t R = 1ull << P.s0;
     const uint64_t slack = (uint64_t)(l2f_parts(P.F1) + 1) * (1ull << l2f_blk_sh()) + 16;
     std::vector<uint64_t> base(nreg + 1, 0);
-    uint64_t acc = 0;
+    uint64_t acc = 0, cmax = 0;
     int i = 0;
     for (uint64_t gi = 0; gi < nreg; gi++) {
         base[gi] = acc;
@@ -243,6 +243,7 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
         const double mean = (double)nkmers * (double)nb / (double)P.p[i];
         uint64_t c = (uint64_t)(mean + g->cap_sigma * sqrt(mean)) + slack;
         acc += (c + 15) & ~15ull;
+        cmax = std::max<uint64_t>(cmax, (c + 15) & ~15ull);
     }
     base[nreg] = acc;
     ensure((void **)&w.reg_base, &w.cap_reg, nreg + 1, 8);
@@ -254,6 +255,7 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
     w.reg_nkmers = nkmers;
     w.reg_sigma = g->cap_sigma;
     w.reg_total = acc;
+    w.reg_max = cmax;
     return acc;
 }
 
@@ -692,7 +694,8 @@ static size_t lds_scatter_w(uint32_t FJ) {
 }
 static int apply_count_threads(const Params &P) { return (1 << P.s0) / 16; }
 template <int KIND>
-static void (*apply_count_kernel(const Params &P))(Params, ApplyArgs) {
+static void (*apply_count_kernel(const Params &P, bool losers = false))(Params, ApplyArgs) {
+    if (losers) return P.s0 == 14 ? k_apply_count<KIND, 1024, true> : k_apply_count<KIND, 512, true>;
     return P.s0 == 14 ? k_apply_count<KIND, 1024> : k_apply_count<KIND, 512>;
 }
 // one 1024-thread workgroup per CU fits the 2^14-bin LDS footprint; two of 512
@@ -837,7 +840,32 @@ struct PassState {
     // coarse-window winner path
     bool coarse = false;
     uint32_t ncw = 0, fpc = 0;
+    // complement mode (losers in the runs, counted per k-mer by k_mark_wf)
+    // and the fine windows of 2^js k-mers (FJ of them) the runs are split into
+    bool losers = false;
+    int js = 0;
+    uint32_t FJ = 0;
 };
+
+// Complement mode for a pass of the coarse path: the runs carry the records
+// that are not their bin's is_new first insert, when those are the fewer --
+// sparse tables, where nearly every insert is a winner (C4 / C5; C2 keeps the
+// winners).  The winner share of a table's inserts is estimated from table 0's
+// zero bins Z before the pass: Z (1 - e^(-m/p)) / m for m inserts into p bins
+// (exactness does not depend on it).  Needs the region's records (<= its
+// l2f capacity) to fit the LDS staging array (2^s0 entries) and at most 15
+// tables (k_mark_wf's 4-bit loser counts); KH_LOSERS=0 / 1 forces it off / on
+// where it applies (development).
+static bool complement_mode(const Graph *g, uint64_t nkmers, bool l2f) {
+    const Params &P = g->prm;
+    static const int force = env_seg("KH_LOSERS", -1);
+    if (force == 0 || g->grouped || P.kind == BIT || P.n > 15 || !l2f || nkmers == 0) return false;
+    if (g->ws.reg_max > (1ull << P.s0)) return false;
+    if (force == 1) return true;
+    const double p0 = (double)P.p[0], m = (double)nkmers;
+    const double z = std::max(0.0, p0 - (double)g->n_occupied);
+    return z * (1.0 - std::exp(-m / p0)) > 0.6 * m;
+}
 
 // The coarse-window winner path (k_apply_count with A.coarse, k_hist_wf,
 // k_scatter_wf, k_mark_wf); KH_WINNERS=1 keeps the per-region winner lists
@@ -888,7 +916,7 @@ static void winners_fine(Graph *g, PassState &ps) {
     KH_HIP(hipMemcpyAsync(w.cmbase, cmbase.data(), (MAX_CW + 1) * 8, hipMemcpyHostToDevice, st));
     KH_HIP(hipMemcpyAsync(w.cnk, cnk.data(), MAX_CW * 4, hipMemcpyHostToDevice, st));
     KH_HIP(hipMemsetAsync(w.mcnt + m, 0, 4, st));
-    const int js = ps.q.js;
+    const int js = ps.js;
     if (!ch.empty())
         TIMED("hist_w", hipLaunchKernelGGL(k_hist_wf, dim3((unsigned)ch.size()), dim3(WF_THREADS), 0, st, A.wco,
                                            (const WChunk *)w.wch, js, ps.fpc, w.mcnt));
@@ -943,9 +971,14 @@ static void pass_apply(Graph *g, PassState &ps, bool l2f) {
     A.wco = win;
     A.cw_cur = nullptr;
     A.dyn = apply_dynamic(g) ? 1 : 0;
+    // complement mode: fine windows of 2^(cjs - 8) k-mers (<= 256 a coarse
+    // window; 4-bit counts of 2^17 k-mers fill k_mark_wf's 128 KB of LDS)
+    ps.losers = ps.coarse && complement_mode(g, nkmers, l2f);
+    ps.js = ps.losers ? A.cjs - 8 : q.js;
+    ps.FJ = (uint32_t)((nkmers + (1ull << ps.js) - 1) >> ps.js);
     if (ps.coarse) {
         ps.ncw = (uint32_t)((nkmers + (1ull << A.cjs) - 1) >> A.cjs);
-        ps.fpc = 1u << (A.cjs - q.js);
+        ps.fpc = 1u << (A.cjs - ps.js);
         if (!w.cw_cur) {
             KH_HIP(hipMalloc((void **)&w.cw_cur, MAX_CW * 8));
             KH_HIP(hipMalloc((void **)&w.cmbase, (MAX_CW + 1) * 8));
@@ -970,10 +1003,10 @@ static void pass_apply(Graph *g, PassState &ps, bool l2f) {
         TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit<APPLY_THREADS>, dim3(agrid), dim3(APPLY_THREADS),
                                               lds_apply(P), st, P, A));
     else if (P.kind == NIBBLE) {
-        TIMED("apply_nibble", hipLaunchKernelGGL(apply_count_kernel<NIBBLE>(P), dim3(agrid_count(g, q)),
+        TIMED("apply_nibble", hipLaunchKernelGGL(apply_count_kernel<NIBBLE>(P, ps.losers), dim3(agrid_count(g, q)),
                                                  dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
     } else {
-        TIMED("apply_byte", hipLaunchKernelGGL(apply_count_kernel<BYTE>(P), dim3(agrid_count(g, q)),
+        TIMED("apply_byte", hipLaunchKernelGGL(apply_count_kernel<BYTE>(P, ps.losers), dim3(agrid_count(g, q)),
                                                dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
     }
     if (bigc)
@@ -1207,9 +1240,11 @@ static void pass_mark_local(Graph *g, PassState &ps, bool want_new) {
     const PassGeo &q = ps.q;
     hipStream_t st = g->stream;
     if (ps.coarse) {
-        TIMED("mark", hipLaunchKernelGGL(k_mark_wf, dim3(q.FJ), dim3(PT_THREADS), ((size_t)1 << q.js) / 8, st, ps.wout,
-                                         w.moff, w.cmbase, w.cnk, ps.fpc, q.js, w.ctr,
-                                         want_new ? w.newbits : nullptr));
+        // LDS: a bit per k-mer (winners) or a 4-bit loser count
+        const size_t lds = ((size_t)1 << ps.js) / (ps.losers ? 2 : 8);
+        TIMED("mark", hipLaunchKernelGGL(k_mark_wf, dim3(ps.FJ), dim3(PT_THREADS), lds, st, ps.wout, w.moff, w.cmbase,
+                                         w.cnk, ps.fpc, ps.js, w.ctr, want_new ? w.newbits : nullptr,
+                                         ps.losers ? (uint32_t)g->prm.n : 0u, ps.nkmers));
         return;
     }
     TIMED("mark", hipLaunchKernelGGL(k_mark, dim3(q.FJ), dim3(PT_THREADS), ((size_t)1 << q.js) / 8, st, ps.wout,
@@ -1818,6 +1853,10 @@ static void set_lds_limits() {
     (void)hipFuncSetAttribute((const void *)k_apply_count<BYTE, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_count<BYTE, 512, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE, 512, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_count<BYTE, 1024, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE, 1024, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_bit<APPLY_THREADS>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_bit<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
 #define KH_LDS_MAX(...) (void)hipFuncSetAttribute((const void *)__VA_ARGS__, hipFuncAttributeMaxDynamicSharedMemorySize, lim)

@@ -147,7 +147,7 @@ struct Workspace {
     // fixed-capacity level 2 (k_scatter_l2f): region g holds [reg_base[g], reg_cur[g])
     uint64_t *reg_base = nullptr;    // [regions + 1] capacity prefix for passes of reg_nkmers k-mers
     uint64_t *reg_cur = nullptr;     // [regions] append cursors
-    uint64_t cap_reg = 0, reg_nkmers = 0, reg_total = 0;
+    uint64_t cap_reg = 0, reg_nkmers = 0, reg_total = 0, reg_max = 0;   // reg_max: largest region capacity
     double reg_sigma = 0, bkt_sigma = 0;          // capacity margins the plans were made with
     // fixed-capacity level 1 (k_scatter_l1f): bucket b holds [bkt_base[b], bkt_cur[b])
     uint64_t *bkt_base = nullptr, *bkt_cur = nullptr;

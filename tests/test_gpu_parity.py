@@ -419,6 +419,37 @@ def test_small_pass_threshold(monkeypatch, cls, small):
         assert dict(zip(keys[:n.value], vals[:n.value])) == o.bigcounts()
 
 
+@pytest.mark.parametrize("cls", ["Countgraph", "SmallCountgraph"])
+def test_tagging_sparse_complement(tmp_path, cls):
+    """consume_seqfile_and_tag (src/oxli/hashgraph.cc:200-320) into sparse
+    tables (3 x ~2e7 bins, passes of ~1e6 k-mers): most inserts are is_new
+    winners, so the apply runs its complement mode (the coarse-window runs
+    carry the losers and k_mark_wf counts them per k-mer), whose per-k-mer new
+    flags place the tags.  Counters, tables, the tag set and the .tagset bytes
+    equal the oracle's."""
+    from khmer_amd import synth
+    n, L = 24000, 100
+    seqs, _ = synth.genomic_batch(0, n, L, 50_000_000)
+    fa = str(tmp_path / "s.fa")
+    with open(fa, "wb") as fh:
+        for r in range(n):
+            fh.write(b">r%d\n%s\n" % (r, seqs[r * L:(r + 1) * L]))
+    sizes = O.get_n_primes_near_x(3, 20000003)
+    g, o = make_pair(cls, 21, sizes)
+    from khmer_amd._lib import lib, check
+    check(lib.kh_graph_set_batch_kmers(g._g, 1000000))
+    got = g.consume_seqfile_and_tag(fa)
+    want = o.consume_fastx(fa, tag=True)
+    assert got == want
+    assert sorted(g._tag_hashes()) == sorted(o.tags())
+    assert len(o.tags()) > 1000
+    assert_same(g, o, "sparse tag")
+    f1, f2 = str(tmp_path / "g.tagset"), str(tmp_path / "o.tagset")
+    g.save_tagset(f1)
+    o.save_tagset(f2)
+    assert open(f1, "rb").read() == open(f2, "rb").read()
+
+
 @pytest.mark.parametrize("cls,k,chunk", [("Nodegraph", 21, 0), ("Nodegraph", 31, 20000), ("Countgraph", 25, 7001)])
 def test_tagging_genomic_multibatch(tmp_path, monkeypatch, cls, k, chunk):
     """consume_seqfile_and_tag (src/oxli/hashgraph.cc:200-320) on a skewed
