@@ -202,9 +202,13 @@ static int l2f_blk_sh() { static const int v = env_seg("KH_L2F_BLK_SH", L2F_BLK_
 static uint32_t l2f_parts(uint32_t F1) {
     static const int v = env_seg("KH_L2F_PARTS", 0);   // development: workgroups per bucket
     if (v > 0) return (uint32_t)v;
-    // ~8K workgroups: few buckets' regions are written at once (measured: 32
-    // per bucket at C2 beats 8 by 3 ms/step, at ~3 % more partial blocks)
-    return std::max<uint32_t>(1, std::min<uint32_t>(32, (8192 + F1 - 1) / F1));
+    // ~8K workgroups, at most 16 per bucket: few buckets' regions are written
+    // at once (round 3: 32 per bucket at C2 beat 8 by 3 ms/step); round 5 at
+    // C2 (240 buckets; profiles/r5/ab_l2_parts.txt, 2 rounds): 16 -> 237.9,
+    // 32 -> 239.6-239.9, 24 -> 240.6-240.8, 12 -> 242.2 ms/step -- 16 and
+    // 32 fill whole waves of one workgroup a CU (3840 / 7680 workgroups on
+    // 256 CUs) and 16 leaves fewer partial blocks
+    return std::max<uint32_t>(1, std::min<uint32_t>(16, (8192 + F1 - 1) / F1));
 }
 static size_t lds_scatter_l2f(const Params &P) { return ((size_t)1 << P.s2) * (8 + 8 + 16 * 8 + 4 + 4 + 2) + 16; }
 // The fixed-capacity path is used when a full region expects >= 512 records
