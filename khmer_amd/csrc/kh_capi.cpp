@@ -1511,7 +1511,7 @@ extern "C" int kh_graph_clear(kh_graph *h) {
         Graph *g = h->g;
         std::lock_guard<std::recursive_mutex> lk(g->mu);
         KH_HIP(hipSetDevice(g->device));
-        KH_HIP(hipMemsetAsync(g->d_tab, 0, g->arena_bytes, g->stream));
+        dev_fill(g->d_tab, 0, g->arena_bytes, g->stream);
         KH_HIP(hipStreamSynchronize(g->stream));
         g->n_unique = g->n_occupied = 0;
         g->bigcounts.clear();

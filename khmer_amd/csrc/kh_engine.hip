@@ -31,6 +31,7 @@
 
 #include "kh_apply.cuh"
 #include "kh_internal.h"
+#include "kh_nearprime.cuh"
 #include "kh_query.cuh"
 
 namespace kh {
@@ -46,6 +47,37 @@ static void ensure(void **p, uint64_t *cap, uint64_t need, size_t elem) {
     *cap = n;
 }
 
+
+// Device fill with 16-byte stores and 64-bit indices, for every range that
+// can be large (tables, record buffers, per-k-mer flags); hipMemsetAsync
+// only below 1 MiB.  Round 5's `bench.py --ablate 16` run faulted ("illegal
+// memory access") in its first pass after a hipMemsetAsync of the whole
+// level-1 buffer (~1.35e11 bytes) -- the only difference from the clean
+// --ablate 0 run of the same build; no memset that large remains
+// (DESIGN.md §5.3).
+__global__ void k_fill16(uint4 *p, uint64_t n, uint4 v) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+void dev_fill(void *p, int v, uint64_t bytes, hipStream_t st) {
+    uint8_t *b = (uint8_t *)p;
+    if (bytes < (1u << 20)) {
+        if (bytes) KH_HIP(hipMemsetAsync(p, v, bytes, st));
+        return;
+    }
+    const uint64_t head = (16 - ((uintptr_t)b & 15)) & 15;
+    if (head) {
+        KH_HIP(hipMemsetAsync(b, v, head, st));
+        b += head;
+        bytes -= head;
+    }
+    const uint64_t n = bytes / 16;
+    const uint32_t w = (uint32_t)(uint8_t)v * 0x01010101u;
+    const unsigned grid = (unsigned)std::min<uint64_t>(n / 256 + 1, 16384);
+    hipLaunchKernelGGL(k_fill16, dim3(grid), dim3(256), 0, st, (uint4 *)b, n, make_uint4(w, w, w, w));
+    KH_HIP(hipGetLastError());
+    if (bytes & 15) KH_HIP(hipMemsetAsync(b + n * 16, v, bytes & 15, st));
+}
 
 static int ceil_log2(uint64_t x) {
     int s = 0;
@@ -228,13 +260,16 @@ static bool l2f_wanted(const Graph *g, uint64_t nkmers) {
 // gets one record per k-mer, spread over its p_i bins) + 8 sigma + the
 // partially filled blocks of every workgroup; uploaded once per pass size.
 // Returns the total capacity in records.
-static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
+// A region is written by the level-2 workgroups of one level-1 bucket (the
+// near-prime level 2, `np`: of two, the spill of the previous bucket's range).
+static uint64_t reg_plan(Graph *g, uint64_t nkmers, bool np = false) {
     Workspace &w = g->ws;
     const Params &P = g->prm;
-    if (w.reg_base && w.reg_nkmers == nkmers && w.reg_sigma == g->cap_sigma) return w.reg_total;
+    if (w.reg_base && w.reg_nkmers == nkmers && w.reg_sigma == g->cap_sigma && w.reg_np == np) return w.reg_total;
     const uint64_t nreg = (uint64_t)P.F1 << P.s2;
     const uint64_t R = 1ull << P.s0;
-    const uint64_t slack = (uint64_t)(l2f_parts(P.F1) + 1) * (1ull << l2f_blk_sh()) + 16;
+    const uint64_t writers = np ? 2 * (uint64_t)l2f_parts(256) + 1 : (uint64_t)l2f_parts(P.F1) + 1;
+    const uint64_t slack = writers * (1ull << l2f_blk_sh()) + 16;
     std::vector<uint64_t> base(nreg + 1, 0);
     uint64_t acc = 0, cmax = 0;
     int i = 0;
@@ -258,6 +293,7 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers) {
     KH_HIP(hipMemcpy(w.reg_base, base.data(), (nreg + 1) * 8, hipMemcpyHostToDevice));
     w.reg_nkmers = nkmers;
     w.reg_sigma = g->cap_sigma;
+    w.reg_np = np;
     w.reg_total = acc;
     w.reg_max = cmax;
     return acc;
@@ -510,6 +546,98 @@ static uint64_t bkt_plan(Graph *g, uint64_t nkmers) {
     w.bkt_sigma = g->cap_sigma;
     w.bkt_total = acc;
     return acc;
+}
+
+// ---- near-prime level 1 / level 2 (kh_nearprime.cuh) ----
+// Taken for 2-bit fixed-length reads into 2-4 unsharded tables whose sizes
+// are close enough that every k-mer's bins lie within a few regions of its
+// bin in the largest table (khmer's get_n_primes_near_x sizes at C2 / C4
+// scale); KH_NEAR_PRIME=0 keeps the per-table level 1 (read in every build:
+// the tests compare both paths).
+static bool np_enabled() { return test_env_int("KH_NEAR_PRIME", 1) != 0; }
+static bool np_geometry(const Graph *g, NPGeo *out) {
+    const Params &P = g->prm;
+    if (!np_enabled() || g->hash != TWOBIT || P.n < 2 || P.n > NP_MAXT || g->k > 26 || use_own_filter(g)) return false;
+    for (int i = 0; i < P.n; i++)
+        if (P.lo[i] != 0 || P.lsz[i] != P.p[i]) return false;
+    NPGeo N{};
+    N.n = P.n;
+    N.s0 = P.s0;
+    N.ablate = P.ablate;
+    const uint64_t R = 1ull << P.s0;
+    uint64_t pm = 0, dmax = 0;
+    for (int i = 0; i < P.n; i++) pm = std::max<uint64_t>(pm, P.p[i]);
+    for (int i = 0; i < P.n; i++) {
+        N.d[i] = pm - P.p[i];
+        N.p[i] = P.p[i];
+        N.rt[i] = (uint32_t)((P.p[i] + R - 1) >> P.s0);
+        N.rbase[i] = (uint32_t)(P.tbase[i] >> P.s0);
+        dmax = std::max<uint64_t>(dmax, N.d[i]);
+        if ((P.tbase[i] & (R - 1)) || (P.tbase[i] >> P.s0) >= (1ull << 32)) return false;
+    }
+    // h < 4^k: the quotient by P, and the farthest a bin lies past r
+    const uint64_t qmax = ((1ull << (2 * g->k)) - 1) / pm;
+    if (qmax >= (1ull << 31)) return false;
+    const unsigned __int128 maxoff = (unsigned __int128)qmax * dmax;
+    if (maxoff + 2 * (unsigned __int128)dmax >= pm) return false;   // r + q d_i < 2 p_i: one subtraction
+    N.rloc = 1024u / (uint32_t)P.n;
+    const uint64_t E = (uint64_t)((maxoff + R - 1) >> P.s0);   // regions of spill past a bucket's range
+    if (E + 1 >= N.rloc / 2) return false;
+    N.rp = N.rloc - (uint32_t)E - 1;   // + 1: a wrapped bin's region index can round up by one
+    const uint64_t Rm = (pm + R - 1) >> P.s0;
+    const uint64_t nb = (Rm + N.rp - 1) / N.rp;
+    if (nb == 0 || nb > 256) return false;   // k_scatter_n1's per-bucket state (one row scan of 4 x 64)
+    N.nb = (uint32_t)nb;
+    N.ob = ceil_log2((uint64_t)N.rp * R + 1);   // an offset is never all ones (the ~0 sentinel)
+    N.pb = N.ob + ceil_log2(qmax + 1);
+    if (N.pb > NP_SLOT_K || 64 - N.pb < 26) return false;
+    N.jlim = 64 - N.pb >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << (64 - N.pb)) - 1);
+    // KH_NP_JLIM (tests): a smaller block index span, so blocks are closed
+    // early and often (np_bkt_plan then allows a closed block per tile)
+    const int jl = test_env_int("KH_NP_JLIM", 0);
+    if (jl >= L1_THREADS * NP_KPT) N.jlim = std::min<uint32_t>(N.jlim, (uint32_t)jl);
+    N.magic = (uint32_t)(((1ull << 32) + N.rp - 1) / N.rp);
+    for (uint64_t rho = 0; rho < Rm; rho++)
+        if ((uint32_t)((rho * N.magic) >> 32) != rho / N.rp) return false;
+    N.pm = pm;
+    N.ipm = 1.0 / (double)pm;
+    *out = N;
+    return true;
+}
+// fixed-length 2-bit reads whose 4096-k-mer tile spans at most NP_TW packed words
+template <class Src>
+static bool np_source(const Src &src) {
+    if constexpr (!std::is_same<Src, SrcTwoBit>::value) return false;
+    else {
+        if (!src.kpr) return false;
+        const uint64_t T = (uint64_t)L1_THREADS * NP_KPT;
+        const uint64_t reads = (T + src.kpr - 1) / src.kpr + 1;
+        const uint64_t span = T + reads * (uint64_t)(src.k - 1) + (uint64_t)src.k;
+        return span / 32 + 3 <= (uint64_t)NP_TW;
+    }
+}
+static uint32_t np_workgroups(const Graph *g, uint64_t nkmers, uint32_t nb) {
+    const uint64_t tiles = (nkmers + (uint64_t)L1_THREADS * NP_KPT - 1) / ((uint64_t)L1_THREADS * NP_KPT);
+    const uint64_t wpc = std::max<uint64_t>(1, std::min<uint64_t>(L1F_WAVES_PER_EU * 4 / (L1_THREADS / 64),
+                                                                   163840 / lds_n1((nb + 3) & ~3u)));
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles / 4 + 1, wpc * device_cus(g)));
+}
+// tiles of a k_scatter_n1 chunk: the k-mers of a k_scatter_l1p chunk
+static uint32_t np_chunk_tiles(const Graph *g) { return std::max<uint32_t>(1, l1f_chunk_tiles(g) / 4); }
+// uniform bucket capacity: a full bucket's expected records + the margin + a
+// partial block per workgroup; returns the records of all buckets
+static uint64_t np_bkt_plan(Graph *g, NPGeo &N, uint64_t nkmers, uint32_t nwg) {
+    Workspace &w = g->ws;
+    const uint64_t BLK = 1ull << l1f_blk_sh();
+    const double mean = (double)nkmers * (double)((uint64_t)N.rp << N.s0) / (double)N.pm;
+    uint64_t cap = (uint64_t)(mean + g->cap_sigma * sqrt(mean)) + (uint64_t)(nwg + 1) * BLK;
+    if (test_env_int("KH_NP_JLIM", 0) > 0)   // at most one closed block per (bucket, tile)
+        cap += (nkmers + L1_THREADS * NP_KPT - 1) / (L1_THREADS * NP_KPT) * BLK;
+    cap = (cap + BLK - 1) / BLK * BLK;
+    N.cap = cap;
+    ensure((void **)&w.np_cur, &w.cap_npcur, N.nb + 1, 8);
+    ensure((void **)&w.np_blkj, &w.cap_blkj, cap / BLK * N.nb + 1, 4);
+    return cap * N.nb;
 }
 
 // KH_CHECK (development): record buffers pre-filled with a sentinel; after
@@ -1076,10 +1204,15 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
     const uint64_t flag_bytes = (nkmers + 15) & ~15ull;
 
     const bool l2f_try = l2f_wanted(g, nkmers);
-    uint64_t cap2 = l2f_try ? reg_plan(g, nkmers) : 0;   // level-2 capacity (records)
+    // near-prime partition: one level-1 record per k-mer (kh_nearprime.cuh)
+    NPGeo npg{};
+    bool np = false;
+    if constexpr (std::is_same<Src, SrcTwoBit>::value)
+        np = l2f_try && np_source(src) && l1f_chunk_tiles(g) >= 1 && np_geometry(g, &npg);
+    uint64_t cap2 = l2f_try ? reg_plan(g, nkmers, np) : 0;   // level-2 capacity (records)
     KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
     if (bigc) {
-        KH_HIP(hipMemsetAsync(w.fullf, 0, flag_bytes, st));
+        dev_fill(w.fullf, 0, flag_bytes, st);
         bcmap_clear(w, st);
     }
 
@@ -1093,11 +1226,24 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
     bool l1f = false;
     uint64_t nrec = 0;   // records this pass writes (exact level 1 only)
     for (;;) {
-        l1f = fast && l1f_ok(g) && (std::is_same<Src, SrcHashes>::value || l1f_direct(P));
-        const bool ownf = fast && !window && use_own_filter(g) && own_l1f_on();
+        np = np && fast;
+        l1f = !np && fast && l1f_ok(g) && (std::is_same<Src, SrcHashes>::value || l1f_direct(P));
+        const bool ownf = !np && fast && !window && use_own_filter(g) && own_l1f_on();
         const uint64_t cap1 = (l1f || ownf) ? bkt_plan(g, nkmers) : 0;
         // level 1
-        if (ownf) {
+        if (np) {
+            if constexpr (std::is_same<Src, SrcTwoBit>::value) {
+                const uint32_t nwg = np_workgroups(g, nkmers, npg.nb);
+                const uint64_t capn = np_bkt_plan(g, npg, nkmers, nwg);
+                ensure_recs(g, std::max(capn, cap2));
+                hipLaunchKernelGGL(k_np_reset, dim3(1), dim3(256), 0, st, w.np_cur, npg.nb, npg.cap);
+                KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, st));   // the chunk queue's head
+                TIMED("scatter_n1", hipLaunchKernelGGL(k_scatter_n1, dim3(nwg), dim3(L1_THREADS),
+                                                       lds_n1((npg.nb + 3) & ~3u), st, npg, src, nkmers, w.np_cur,
+                                                       w.rec1, w.np_blkj, w.ctr, l1f_blk_sh(), 0u,
+                                                       np_chunk_tiles(g)));
+            }
+        } else if (ownf) {
             ensure_recs(g, std::max(cap1, cap2));
             hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)((F1 + 255) / 256)), dim3(256), 0, st, w.bkt_base,
                                (unsigned long long *)w.bkt_cur, (uint64_t)F1);
@@ -1116,7 +1262,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
             }
         } else if (l1f) {
             ensure_recs(g, std::max(cap1, cap2));
-            if (KH_ABL(P, 16)) KH_HIP(hipMemsetAsync(w.rec1, 0xFF, w.cap_recs * 8, st));   // timing only
+            if (KH_ABL(P, 16)) dev_fill(w.rec1, 0xFF, w.cap_recs * 8, st);   // timing only
             hipLaunchKernelGGL(k_reg_reset, dim3((unsigned)((F1 + 255) / 256)), dim3(256), 0, st, w.bkt_base,
                                (unsigned long long *)w.bkt_cur, (uint64_t)F1);
             launch_l1f(g, src, nkmers, window, 0u);
@@ -1133,8 +1279,8 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
                                                 nch, w.moff, w.mcnt, w.off1, w.ch2));
             ensure_recs(g, std::max(nrec, cap2));
             if (check_mode()) {
-                KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
-                KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
+                dev_fill(w.rec1, 0xFF, nrec * 8, st);
+                dev_fill(w.rec2, 0xFF, nrec * 8, st);
             }
             SrcHashes rs{};
             rs.h = w.frec;
@@ -1153,8 +1299,8 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
             KH_HIP(hipStreamSynchronize(st));
             ensure_recs(g, std::max(nrec, cap2));
             if (check_mode()) {
-                KH_HIP(hipMemsetAsync(w.rec1, 0xFF, nrec * 8, st));
-                KH_HIP(hipMemsetAsync(w.rec2, 0xFF, nrec * 8, st));
+                dev_fill(w.rec1, 0xFF, nrec * 8, st);
+                dev_fill(w.rec2, 0xFF, nrec * 8, st);
             }
             // Table groups of up to 8 per launch.  Above 1024 buckets (C4, C5:
             // 1908), each launch takes the tables whose buckets fit 1024 and
@@ -1198,13 +1344,22 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
             const bool bkt = l1f || ownf;   // level 1 went into fixed-capacity buckets
             const uint64_t *bs = bkt ? w.bkt_base : w.off1;
             const uint64_t *be = bkt ? w.bkt_cur : w.off1 + 1;
-            TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(F1 * parts)),
-                                                   dim3(PT_THREADS), lds_scatter_l2f(P), st, (uint32_t)F1, P.s0,
-                                                   P.s2, parts, bs, be, w.reg_base, (unsigned long long *)w.reg_cur,
-                                                   w.rec1, w.rec2, w.ctr, l2f_blk_sh()));
+            if (np) {
+                const uint32_t nparts = l2f_parts(npg.nb);
+                TIMED("scatter_n2", hipLaunchKernelGGL(n2_kernel(npg.n), dim3(npg.nb * nparts), dim3(PT_THREADS),
+                                                       lds_scatter_n2(npg), st, npg, nparts, w.np_cur, w.np_blkj,
+                                                       l1f_blk_sh(), w.reg_base, (unsigned long long *)w.reg_cur,
+                                                       w.rec1, w.rec2, w.ctr, l2f_blk_sh()));
+            } else {
+                TIMED("scatter_l2", hipLaunchKernelGGL((k_scatter_l2f<PT_THREADS, L2_RPT>), dim3((unsigned)(F1 * parts)),
+                                                       dim3(PT_THREADS), lds_scatter_l2f(P), st, (uint32_t)F1, P.s0,
+                                                       P.s2, parts, bs, be, w.reg_base, (unsigned long long *)w.reg_cur,
+                                                       w.rec1, w.rec2, w.ctr, l2f_blk_sh()));
+            }
             uint64_t err = 0;
             KH_HIP(hipMemcpyAsync(&err, w.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
             KH_HIP(hipStreamSynchronize(st));
+            if (err & 16) fail(KH_EDEVICE, "near-prime level 2: a bin outside its bucket's regions");
             if (err & 12) {   // a bucket or region overflowed (the tables are untouched until apply)
                 KH_HIP(hipMemsetAsync(w.ctr + CTR_ERR, 0, 8, st));
                 // redo the pass on the fast path with 3x the capacity margin
@@ -1212,7 +1367,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
                 // exactly (histogram path), and the next 8 passes too
                 if (g->cap_sigma < 72.0 && recs_fit(g, nkmers, g->cap_sigma * 3.0)) {
                     g->cap_sigma *= 3.0;
-                    cap2 = reg_plan(g, nkmers);
+                    cap2 = reg_plan(g, nkmers, np);
                     continue;
                 }
                 fast = false;
@@ -1902,6 +2057,10 @@ static void set_lds_limits() {
     KH_LDS_MAX((k_own_filter<SrcHashes, 16>));
     KH_LDS_MAX((k_scatter_w<PT_THREADS, 2>));
     KH_LDS_MAX((k_scatter_l1p<2>));
+    KH_LDS_MAX(k_scatter_n1);
+    KH_LDS_MAX((k_scatter_n2<PT_THREADS, 2>));
+    KH_LDS_MAX((k_scatter_n2<PT_THREADS, 3>));
+    KH_LDS_MAX((k_scatter_n2<PT_THREADS, 4>));
     KH_LDS_MAX((k_apply_delta<BYTE, 1024>));
     KH_LDS_MAX((k_apply_delta<NIBBLE, 1024>));
     KH_LDS_MAX((k_apply_delta<BIT, 1024>));
@@ -1972,7 +2131,7 @@ static Graph *graph_build(int kind, int hash, int k, const uint64_t *sizes, int 
     }
     KH_HIP(e);
     KH_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
-    KH_HIP(hipMemsetAsync(g->d_tab, 0, arena, g->stream));
+    dev_fill(g->d_tab, 0, arena, g->stream);
     KH_HIP(hipStreamSynchronize(g->stream));
     return g.release();
 }
@@ -1988,7 +2147,7 @@ Graph::~Graph() {
     void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.fullf, w.newbits, w.bc, w.bcn, w.bck, w.bcv,
                     w.off1, w.ch2, w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.xseg, w.reg_base, w.reg_cur, w.bkt_base, w.bkt_cur, w.ctr, w.d_words, w.d_koff, w.d_bytes,
                     w.q_hashes, w.q_counts, w.frec, w.fcount, w.d_rbytes, w.sm_flags, w.sm_hash, w.cw_cur, w.cmbase,
-                    w.cnk, w.wch};
+                    w.cnk, w.wch, w.np_cur, w.np_blkj};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (w.h_ctr) (void)hipHostFree(w.h_ctr);
@@ -2472,7 +2631,7 @@ static void group_merge_full(ShardGroup *G, std::vector<PassState> &ps) {
         auto &lc = G->loc[0];
         ensure((void **)&lc.fall, &lc.cap_fall, (uint64_t)W * mx, 8);
         coll_allgather_u64(G, g->stream, lc.flist, lc.fall, mx);
-        KH_HIP(hipMemsetAsync(g->ws.fullf, 0, nkb, g->stream));
+        dev_fill(g->ws.fullf, 0, nkb, g->stream);
         hipLaunchKernelGGL(k_full_scatter, dim3(2048), dim3(256), 0, g->stream, lc.fall, (uint64_t)W * mx,
                            g->ws.fullf);
     } else {
@@ -2480,7 +2639,7 @@ static void group_merge_full(ShardGroup *G, std::vector<PassState> &ps) {
         for (int l = 0; l < NL; l++) {
             Graph *g = G->shards[l];
             KH_HIP(hipSetDevice(g->device));
-            KH_HIP(hipMemsetAsync(g->ws.fullf, 0, nkb, g->stream));
+            dev_fill(g->ws.fullf, 0, nkb, g->stream);
             for (int s = 0; s < W; s++)
                 if (cnt[s])
                     hipLaunchKernelGGL(k_full_scatter, dim3(2048), dim3(256), 0, g->stream, G->loc[s].flist, cnt[s],
@@ -2725,7 +2884,7 @@ static PassState a2a_owner_pass(ShardGroup *G, int l, const std::vector<uint64_t
     ws_prepare(g, ps.q);
     KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
     if (ps.bigc) {
-        KH_HIP(hipMemsetAsync(w.fullf, 0, (nk + 15) & ~15ull, st));
+        dev_fill(w.fullf, 0, (nk + 15) & ~15ull, st);
         bcmap_clear(w, st);
     }
     const uint64_t nseg = a2a_segments(G, l, meta, rb);
@@ -3530,7 +3689,7 @@ static void group_median_a2a(ShardGroup *G, const GroupReads &R, const QueryOut 
             auto &lc = G->loc[l];
             KH_HIP(hipSetDevice(g->device));
             const uint64_t nseg = a2a_segments(G, l, meta, rb[l]);
-            KH_HIP(hipMemsetAsync(lc.q8, 0xFF, (nk + 3) & ~3ull, g->stream));
+            dev_fill(lc.q8, 0xFF, (nk + 3) & ~3ull, g->stream);
             if (nseg)
                 TIMED("lookup", hipLaunchKernelGGL(k_lookup_min, dim3((unsigned)(nseg * PARTS)), dim3(256), 0,
                                                    g->stream, g->prm, g->d_tab, g->ws.rec1, lc.seg,

@@ -148,6 +148,12 @@ struct Workspace {
     uint64_t *reg_base = nullptr;    // [regions + 1] capacity prefix for passes of reg_nkmers k-mers
     uint64_t *reg_cur = nullptr;     // [regions] append cursors
     uint64_t cap_reg = 0, reg_nkmers = 0, reg_total = 0, reg_max = 0;   // reg_max: largest region capacity
+    bool reg_np = false;             // planned for the near-prime level 2 (two writing buckets a region)
+    // near-prime level 1 (kh_nearprime.cuh): bucket d holds [d cap, np_cur[d]);
+    // np_blkj[block] = the k-mer index base of a level-1 block
+    unsigned long long *np_cur = nullptr;
+    uint32_t *np_blkj = nullptr;
+    uint64_t cap_npcur = 0, cap_blkj = 0;
     double reg_sigma = 0, bkt_sigma = 0;          // capacity margins the plans were made with
     // fixed-capacity level 1 (k_scatter_l1f): bucket b holds [bkt_base[b], bkt_cur[b])
     uint64_t *bkt_base = nullptr, *bkt_cur = nullptr;
@@ -335,6 +341,9 @@ inline uint64_t shard_lo(uint64_t p, int world, int r) {
     return x & ~7ull;
 }
 void graph_zero_counters(Graph *g);
+// fill `bytes` bytes of device memory at p with v on stream st (64-bit
+// indices, 16-byte stores; large ranges never go through hipMemsetAsync)
+void dev_fill(void *p, int v, uint64_t bytes, hipStream_t st);
 void graph_prepare_params(Graph *g);
 // run one device pipeline pass over a device-resident batch.
 // Optional outputs: per-k-mer is-new flags and hashes (device pointers filled

@@ -1061,6 +1061,7 @@ __global__ void __launch_bounds__(L1_THREADS, L1F_WAVES_PER_EU) k_scatter_l1p(Pa
                 const uint64_t v0 = ((jbase + j0 + (bj0 & 0xFFFFu)) << 32) | (uint32_t)sp.x;
                 const uint64_t v1 = ((jbase + j0 + (bj1 & 0xFFFFu)) << 32) | (uint32_t)sp.y;
                 const uint64_t o = (q >= ql.x ? dv.y : dv.x) + q;
+                if (KH_ABL(P, 16)) continue;   // timing only: no run writes (as k_scatter_l1f)
                 if (q < ql.y) {
                     if (r0 && r1) *(ulonglong2 *)(rec + o) = make_ulonglong2(v0, v1);
                     else if (r0) rec[o] = v0;
