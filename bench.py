@@ -12,10 +12,13 @@ finalize), i.e. the whole hot path over the whole batch.
 Multi-GPU (one rank per GPU; `--gpus N` starts the N rank processes itself
 unless a launcher set WORLD_SIZE): every table is split into G contiguous bin
 ranges, one per rank.  Every rank generates its own 50M
-reads (weak scaling).  Default group mode "exchange" (Option A): each rank
-hashes only its own reads into level-1 buckets and sends every bucket to its
-owner over RCCL/xGMI (grouped send/recv); "broadcast" (Option B): each rank's
-reads are broadcast and every rank hashes every k-mer, keeping its own bins'
+reads (weak scaling).  Default group mode "delta": every rank counts its own
+reads into full-size delta tables, the owners turn every rank's deltas of
+their slice into per-rank prefixes (table bytes over RCCL/xGMI, grouped
+send/recv) and each rank re-applies its reads over its prefix; "exchange"
+(Option A): each rank hashes only its own reads into level-1 buckets and
+sends every bucket to its owner; "broadcast" (Option B): each rank's reads
+are broadcast and every rank hashes every k-mer, keeping its own bins'
 updates.  value = all ranks' k-mers / max time.
 
 Prints ONE JSON line (rank 0).

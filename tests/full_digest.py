@@ -46,6 +46,20 @@ CONFIGS = {
     # over G ranks): 4 x 8e9 bytes; 32 GB of host memory for the oracle
     "c4_50m": dict(kind=1, hash=0, k=21, n=4, x=8e9, reads=50_000_000, L=150, bigcount=True,
                    genome=0, batch_kmers=3200 << 20),
+    # the secondary bench lines' own workloads (tools/bench_modes.sh; VERDICT
+    # r5 #3): C3, C5 and C5M at 50M reads, C5M at BASELINE configs[4]'s 500M
+    # (a read-count prefix pair: one oracle pass with --snapshots), and C2's
+    # genomic stream over a 1e8-base genome
+    "c3_50m": dict(kind=2, hash=0, k=31, n=4, x=4e9, reads=50_000_000, L=150, bigcount=False,
+                   genome=0, batch_kmers=3200 << 20),
+    "c5_50m": dict(kind=7, hash=0, k=31, n=4, x=8e9, reads=50_000_000, L=150, bigcount=False,
+                   genome=0, batch_kmers=3200 << 20),
+    "c5m_50m": dict(kind=7, hash=1, k=51, n=4, x=8e9, reads=50_000_000, L=150, bigcount=False,
+                    genome=0, batch_kmers=3200 << 20),
+    "c5m_500m": dict(kind=7, hash=1, k=51, n=4, x=8e9, reads=500_000_000, L=150, bigcount=False,
+                     genome=0, batch_kmers=3200 << 20),
+    "genomic_c2_50m": dict(kind=1, hash=0, k=21, n=4, x=1e9, reads=50_000_000, L=150, bigcount=True,
+                           genome=100_000_000, batch_kmers=3200 << 20),
 }
 
 # Weak-scaling streams of `bench.py --gpus G` (C2, 50M reads per rank: rank r
@@ -141,7 +155,8 @@ def median_digest(med, avg, sd):
 
 # get_median_count digests over the first MEDIAN_READS reads of the stream,
 # for the configurations whose query path the bench measures (C5 / C5M)
-MEDIAN_READS = {"c5_shape": 1_000_000, "c5m_shape": 1_000_000, "c5_genomic": 1_000_000, "c5m_genomic": 1_000_000}
+MEDIAN_READS = {"c5_shape": 1_000_000, "c5m_shape": 1_000_000, "c5_genomic": 1_000_000, "c5m_genomic": 1_000_000,
+                "c5_50m": 1_000_000, "c5m_50m": 1_000_000}
 
 
 def fixture_path(name):
