@@ -1048,6 +1048,150 @@ uint64_t or_consume_synth(or_table *t, uint64_t seed, uint64_t genome, uint64_t 
     return total;
 }
 
+/* The same stream-order consume spread over threads, for the full-size golden
+ * fixtures (5e10 adds into 16-32 GB tables: one cache/TLB miss per (k-mer,
+ * table) makes the single-threaded loop ~2 M k-mers/s).  Nothing about the
+ * result changes:
+ *  - the reads of a super-group are synthesised and hashed by worker threads
+ *    (pure functions of the read index) into contiguous per-worker slices, so
+ *    the concatenation is the stream order;
+ *  - table i is updated by its own thread, k-mer by k-mer in stream order, so
+ *    every bin sees exactly the sequence of values it sees in add_b; the
+ *    thread records per k-mer whether its bin was zero (is_new, occupied) and
+ *    whether it was full (ByteStorage's n_full);
+ *  - the calling thread then combines the flags in stream order: unique and
+ *    occupied as add_b counts them, and the bigcount increments (saturating
+ *    increments of one key per k-mer: storage.hh:606-616).
+ * The previous super-group's table updates overlap the next one's hashing. */
+#define SG_READS 16384
+struct synth_job {
+    const or_table *t; uint64_t seed, genome, r0, r1; int L;
+    uint64_t *hs; uint64_t n;
+};
+static void *synth_hash_worker(void *arg) {
+    struct synth_job *j = arg;
+    char *buf = malloc((size_t)j->L + 1);
+    struct sink_h sk = {j->hs, 0};
+    for (uint64_t r = j->r0; r < j->r1; r++) {
+        if (j->genome) or_synth_genomic_read(j->seed, j->genome, r, j->L, buf);
+        else or_synth_read(j->seed, r, j->L, buf);
+        iterate_kmers(j->t, buf, (size_t)j->L, cb_sink, &sk);
+    }
+    j->n = sk.n;
+    free(buf);
+    return NULL;
+}
+struct table_job {
+    or_table *t; int i; const uint64_t *hs; uint64_t nh; uint8_t *flags;   /* bit 0: was zero, bit 1: full */
+};
+static void *table_add_worker(void *arg) {
+    struct table_job *j = arg;
+    or_table *t = j->t;
+    const uint64_t p = t->sizes[j->i];
+    uint8_t *tab = t->tab[j->i];
+    const uint64_t *hs = j->hs;
+    for (uint64_t x = 0; x < j->nh; x++) {
+        if (x + PF_AHEAD < j->nh) {
+            const uint64_t b = hs[x + PF_AHEAD] % p;
+            __builtin_prefetch(tab + (t->kind == OR_BIT ? b / 8 : t->kind == OR_NIBBLE ? b / 2 : b), 1, 0);
+        }
+        const uint64_t bin = hs[x] % p;
+        uint8_t f = 0;
+        if (t->kind == OR_BIT) {                         /* storage.hh:172-199 */
+            const uint8_t bit = (uint8_t)(1u << (bin % 8));
+            const uint8_t orig = tab[bin / 8];
+            tab[bin / 8] = orig | bit;
+            f = !(orig & bit);
+        } else if (t->kind == OR_NIBBLE) {               /* storage.hh:320-359 */
+            const uint64_t idx = bin / 2;
+            const uint8_t mask = (bin % 2) ? 0x0F : 0xF0;
+            const int shift = (bin % 2) ? 0 : 4;
+            const uint8_t cur = (uint8_t)((tab[idx] & mask) >> shift);
+            f = cur == 0;
+            if (cur != 15) tab[idx] = (uint8_t)((tab[idx] & ~mask) | ((uint8_t)((cur + 1) << shift) & mask));
+        } else {                                         /* storage.hh:571-624 */
+            const uint8_t cur = tab[bin];
+            f = cur == 0;
+            if (cur < MAX_KCOUNT) tab[bin] = (uint8_t)(cur + 1);
+            else f |= 2;
+        }
+        j->flags[x] = f;
+    }
+    return NULL;
+}
+uint64_t or_consume_synth_mt(or_table *t, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L,
+                             int nthreads) {
+    if (nthreads < 2) return or_consume_synth(t, seed, genome, r0, nreads, L);
+    if (nthreads > 64) nthreads = 64;
+    const int n = t->n;
+    const uint64_t per = (uint64_t)(L + 1) * SG_READS;
+    uint64_t *hbuf[2] = {malloc(per * 8), malloc(per * 8)};
+    uint64_t *hcat = malloc(per * 8);
+    uint8_t *flags = malloc(per * (uint64_t)n);
+    struct synth_job jobs[2][64];
+    struct table_job tj[64];
+    pthread_t th[64], tt[64];
+    uint64_t total = 0, nprev = 0;
+    const uint64_t end = r0 + nreads;
+    int cur = 0;
+    for (uint64_t g = r0;; g += SG_READS) {
+        const uint64_t ge = g < end ? (g + SG_READS < end ? g + SG_READS : end) : g;
+        int nt = 0;
+        if (g < end) {
+            uint64_t off = 0;
+            for (int i = 0; i < nthreads; i++) {
+                struct synth_job *j = &jobs[cur][i];
+                j->t = t; j->seed = seed; j->genome = genome; j->L = L;
+                j->r0 = g + (ge - g) * (uint64_t)i / (uint64_t)nthreads;
+                j->r1 = g + (ge - g) * (uint64_t)(i + 1) / (uint64_t)nthreads;
+                j->hs = hbuf[cur] + off;
+                off += (j->r1 - j->r0) * (uint64_t)(L + 1);
+                pthread_create(&th[i], NULL, synth_hash_worker, j);
+                nt++;
+            }
+        }
+        if (nprev) {   /* the previous super-group (hashes in hcat, stream order) */
+            for (int i = 0; i < n; i++) {
+                tj[i] = (struct table_job){t, i, hcat, nprev, flags + (uint64_t)i * per};
+                pthread_create(&tt[i], NULL, table_add_worker, &tj[i]);
+            }
+            for (int i = 0; i < n; i++) pthread_join(tt[i], NULL);
+            for (uint64_t x = 0; x < nprev; x++) {
+                int is_new = 0, nfull = 0;
+                for (int i = 0; i < n; i++) {
+                    const uint8_t f = flags[(uint64_t)i * per + x];
+                    if ((f & 1) && !is_new) {
+                        is_new = 1;
+                        if (i == 0) t->occupied++;
+                    }
+                    nfull += (f >> 1) & 1;
+                }
+                if (t->kind == OR_BYTE && nfull == n && t->use_bigcount) {
+                    int created;
+                    const uint64_t s = map_slot(&t->bigcounts, hcat[x], &created);
+                    if (t->bigcounts.vals[s] == 0) t->bigcounts.vals[s] = MAX_KCOUNT + 1;
+                    else if (t->bigcounts.vals[s] < MAX_BIGCOUNT) t->bigcounts.vals[s]++;
+                }
+                if (is_new) t->unique++;
+            }
+            total += nprev;
+            nprev = 0;
+        }
+        for (int i = 0; i < nt; i++) pthread_join(th[i], NULL);
+        if (g >= end) break;
+        for (int i = 0; i < nthreads; i++) {   /* gather the slices in stream order */
+            memcpy(hcat + nprev, jobs[cur][i].hs, jobs[cur][i].n * 8);
+            nprev += jobs[cur][i].n;
+        }
+        cur ^= 1;
+    }
+    free(hbuf[0]);
+    free(hbuf[1]);
+    free(hcat);
+    free(flags);
+    return total;
+}
+
 /* get_median_count (or_median, src/oxli/hashtable.cc:299-328) of reads
  * r0..r0+nreads-1 of a synthetic stream, one output triple per read (the
  * golden fixtures' query digests) */

@@ -111,6 +111,8 @@ uint64_t  or_consume_batch_mt(or_table *t, const char *seqs, const uint64_t *off
 void      or_synth_read(uint64_t seed, uint64_t r, int L, char *out /* L+1 */);
 void      or_synth_genomic_read(uint64_t seed, uint64_t genome, uint64_t r, int L, char *out /* L+1 */);
 uint64_t  or_consume_synth(or_table *t, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L);
+uint64_t  or_consume_synth_mt(or_table *t, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L,
+                              int nthreads);
 int       or_median_synth(const or_table *t, uint64_t seed, uint64_t genome, uint64_t r0, uint64_t nreads, int L,
                           uint16_t *med, float *avg, float *sd);
 

@@ -76,6 +76,7 @@ def lib():
             "or_synth_read": (None, [u64, u64, i32, ctypes.c_char_p]),
             "or_synth_genomic_read": (None, [u64, u64, u64, i32, ctypes.c_char_p]),
             "or_consume_synth": (u64, [P, u64, u64, u64, u64, i32]),
+            "or_consume_synth_mt": (u64, [P, u64, u64, u64, u64, i32, i32]),
             "or_median_synth": (i32, [P, u64, u64, u64, u64, i32, P, P, P]),
         }
         for name, (res, args) in sig.items():
@@ -208,9 +209,12 @@ class Table:
             return lib().or_consume_batch_mt(self._h, seqs, arr, len(offs) - 1, threads)
         return lib().or_consume_batch(self._h, seqs, arr, len(offs) - 1)
 
-    def consume_synth(self, seed, r0, nreads, length, genome=0):
+    def consume_synth(self, seed, r0, nreads, length, genome=0, threads=1):
         """Consume reads r0.. of the benchmark's synthetic stream (khmer_amd/synth.py),
-        in stream order; genome > 0 selects the genomic stream."""
+        in stream order; genome > 0 selects the genomic stream.  threads > 1
+        hashes on worker threads, the adds stay in stream order (same result)."""
+        if threads > 1:
+            return lib().or_consume_synth_mt(self._h, seed, genome, r0, nreads, length, threads)
         return lib().or_consume_synth(self._h, seed, genome, r0, nreads, length)
 
     def median_synth(self, seed, r0, nreads, length, genome=0):

@@ -6,6 +6,12 @@ counters and the bigcount-map digest of one tests/full_digest.CONFIGS entry.
 
     python tests/golden/make_full_fixtures.py c2_full c3_shape ...
     python tests/golden/make_full_fixtures.py --snapshots c2_w2 c2_w4 c2_w8
+    KH_FIXTURE_THREADS=6 python tests/golden/make_full_fixtures.py c5m_500m
+
+KH_FIXTURE_THREADS > 1: the oracle's or_consume_synth_mt (hashing on worker
+threads, one thread per table, flags combined in stream order: the same
+tables and counters, tests/test_oracle_mt_cpu.py) -- ~10 M k-mers/s for the
+Murmur k=51 stream instead of ~2.3 M.
 
 --snapshots: configurations that differ only in their read count and are
 consumed in stream order (no exchange interleave) are prefixes of one stream;
@@ -24,6 +30,8 @@ sys.path.insert(0, ROOT)
 from oracle import oracle as O  # noqa: E402
 from khmer_amd import synth  # noqa: E402
 from tests import full_digest as FD  # noqa: E402
+
+THREADS = int(os.environ.get("KH_FIXTURE_THREADS", "1"))
 
 
 def _table(c):
@@ -66,8 +74,8 @@ def make(name):
     t0 = time.time()
     kmers = 0
     for r0, nr in FD.stream_chunks(c):
-        kmers += t.consume_synth(synth.SEED, r0, nr, c["L"], genome=c["genome"])
-    _write(name, c, t, sizes, kmers, time.time() - t0)
+        kmers += t.consume_synth(synth.SEED, r0, nr, c["L"], genome=c["genome"], threads=THREADS)
+    _write(name, c, t, sizes, kmers, time.time() - t0, ", %d hash threads" % THREADS if THREADS > 1 else "")
 
 
 def make_snapshots(names):
@@ -85,7 +93,7 @@ def make_snapshots(names):
     kmers, r0, step = 0, 0, 1_000_000
     while marks:
         nr = min(step, marks[0][0] - r0)
-        kmers += t.consume_synth(synth.SEED, r0, nr, base["L"], genome=base["genome"])
+        kmers += t.consume_synth(synth.SEED, r0, nr, base["L"], genome=base["genome"], threads=THREADS)
         r0 += nr
         while marks and marks[0][0] == r0:
             _, n = marks.pop(0)
