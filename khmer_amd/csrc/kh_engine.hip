@@ -262,14 +262,21 @@ static bool l2f_wanted(const Graph *g, uint64_t nkmers) {
 // Returns the total capacity in records.
 // A region is written by the level-2 workgroups of one level-1 bucket (the
 // near-prime level 2, `np`: of two, the spill of the previous bucket's range).
-static uint64_t reg_plan(Graph *g, uint64_t nkmers, bool np = false) {
+// np2 (near-prime level 2, kh_nearprime.cuh): a region's first E + 1
+// regions of each bucket range also take the previous bucket's spill, so
+// twice the writing workgroups may leave a partial block there
+static uint64_t reg_plan(Graph *g, uint64_t nkmers, const NPGeo *np2 = nullptr) {
     Workspace &w = g->ws;
     const Params &P = g->prm;
-    if (w.reg_base && w.reg_nkmers == nkmers && w.reg_sigma == g->cap_sigma && w.reg_np == np) return w.reg_total;
+    const uint32_t nparts = np2 ? l2f_parts(np2->nb) : 0;
+    const uint64_t npkey = np2 ? ((uint64_t)np2->rp << 40 | (uint64_t)np2->rloc << 20 | nparts) : 0;
+    if (w.reg_base && w.reg_nkmers == nkmers && w.reg_sigma == g->cap_sigma && w.reg_np == npkey) return w.reg_total;
     const uint64_t nreg = (uint64_t)P.F1 << P.s2;
     const uint64_t R = 1ull << P.s0;
-    const uint64_t writers = np ? 2 * (uint64_t)l2f_parts(256) + 1 : (uint64_t)l2f_parts(P.F1) + 1;
-    const uint64_t slack = writers * (1ull << l2f_blk_sh()) + 16;
+    const uint64_t blk = 1ull << l2f_blk_sh();
+    const uint64_t slack1 = np2 ? (uint64_t)(nparts + 1) * blk + 16 : (uint64_t)(l2f_parts(P.F1) + 1) * blk + 16;
+    const uint64_t slack2 = np2 ? (uint64_t)(2 * nparts + 1) * blk + 16 : slack1;
+    const uint64_t E = np2 ? np2->rloc - np2->rp - 1 : 0;
     std::vector<uint64_t> base(nreg + 1, 0);
     uint64_t acc = 0, cmax = 0;
     int i = 0;
@@ -280,6 +287,8 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers, bool np = false) {
         if (lo >= P.tbase[i] + P.lsz[i]) continue;   // padding up to the next bucket boundary
         const uint64_t nb = std::min<uint64_t>(R, P.tbase[i] + P.lsz[i] - lo);
         const double mean = (double)nkmers * (double)nb / (double)P.p[i];
+        const uint64_t rho = (lo - P.tbase[i]) >> P.s0;
+        const uint64_t slack = np2 && rho % np2->rp <= E ? slack2 : slack1;
         uint64_t c = (uint64_t)(mean + g->cap_sigma * sqrt(mean)) + slack;
         acc += (c + 15) & ~15ull;
         cmax = std::max<uint64_t>(cmax, (c + 15) & ~15ull);
@@ -293,7 +302,7 @@ static uint64_t reg_plan(Graph *g, uint64_t nkmers, bool np = false) {
     KH_HIP(hipMemcpy(w.reg_base, base.data(), (nreg + 1) * 8, hipMemcpyHostToDevice));
     w.reg_nkmers = nkmers;
     w.reg_sigma = g->cap_sigma;
-    w.reg_np = np;
+    w.reg_np = npkey;
     w.reg_total = acc;
     w.reg_max = cmax;
     return acc;
@@ -555,8 +564,20 @@ static uint64_t bkt_plan(Graph *g, uint64_t nkmers) {
 // scale); KH_NEAR_PRIME=0 keeps the per-table level 1 (read in every build:
 // the tests compare both paths).
 static bool np_enabled() { return test_env_int("KH_NEAR_PRIME", 1) != 0; }
-static bool np_geometry(const Graph *g, NPGeo *out) {
+// magic division check: (rho * magic) >> 32 == rho / d for every rho < n
+static bool np_magic_ok(uint64_t n, uint32_t d, uint32_t magic) {
+    for (uint64_t rho = 0; rho < n; rho++)
+        if ((uint32_t)((rho * magic) >> 32) != rho / d) return false;
+    return true;
+}
+// *fine: F = 0 for two levels; otherwise the level-1b split of each of the
+// out->nb coarse buckets (out->rp = F x fine R') into F fine buckets, taken
+// when the two-level geometry needs more than 256 level-1 buckets (C4) and a
+// fine record (j << 32 | q << ob_f | offset) fits 64 bits.  KH_NP_L1MAX
+// (tests) lowers the 256, so small tables take three levels too.
+static bool np_geometry(const Graph *g, NPGeo *out, NPFine *fine) {
     const Params &P = g->prm;
+    *fine = NPFine{};
     if (!np_enabled() || g->hash != TWOBIT || P.n < 2 || P.n > NP_MAXT || g->k > 26 || use_own_filter(g)) return false;
     for (int i = 0; i < P.n; i++)
         if (P.lo[i] != 0 || P.lsz[i] != P.p[i]) return false;
@@ -583,10 +604,29 @@ static bool np_geometry(const Graph *g, NPGeo *out) {
     N.rloc = 1024u / (uint32_t)P.n;
     const uint64_t E = (uint64_t)((maxoff + R - 1) >> P.s0);   // regions of spill past a bucket's range
     if (E + 1 >= N.rloc / 2) return false;
-    N.rp = N.rloc - (uint32_t)E - 1;   // + 1: a wrapped bin's region index can round up by one
+    const uint32_t rpf = N.rloc - (uint32_t)E - 1;   // + 1: a wrapped bin's region index can round up by one
     const uint64_t Rm = (pm + R - 1) >> P.s0;
+    const uint64_t lim = (uint64_t)std::max(1, std::min(256, test_env_int("KH_NP_L1MAX", 256)));
+    uint64_t F = 1, rp = rpf;
+    if ((Rm + rpf - 1) / rpf > lim) {   // three levels
+        // fine buckets small enough that q << ob_f | offset fits 32 bits
+        const int qb = ceil_log2(qmax + 1);
+        if (qb + P.s0 + 1 > 32) return false;
+        rp = std::min<uint64_t>(rpf, ((1ull << (32 - qb)) - 1) / R);
+        F = (Rm + rp * lim - 1) / (rp * lim);
+        const int obf = ceil_log2(rp * R + 1);
+        if (F > N1B_MAXF || obf + qb > 32) return false;
+        const uint32_t mf = (uint32_t)(((1ull << 32) + rp - 1) / rp);
+        if (!np_magic_ok(rp * F, (uint32_t)rp, mf)) return false;
+        fine->F = (uint32_t)F;
+        fine->rp = (uint32_t)rp;
+        fine->magic = mf;
+        fine->ob = obf;
+        fine->rloc = (uint32_t)(rp + E + 1);   // level-2 destinations per table
+    }
+    N.rp = (uint32_t)(rp * F);
     const uint64_t nb = (Rm + N.rp - 1) / N.rp;
-    if (nb == 0 || nb > 256) return false;   // k_scatter_n1's per-bucket state (one row scan of 4 x 64)
+    if (nb == 0 || nb > lim) return false;   // k_scatter_n1's per-bucket state (one row scan of 4 x 64)
     N.nb = (uint32_t)nb;
     N.ob = ceil_log2((uint64_t)N.rp * R + 1);   // an offset is never all ones (the ~0 sentinel)
     N.pb = N.ob + ceil_log2(qmax + 1);
@@ -597,12 +637,33 @@ static bool np_geometry(const Graph *g, NPGeo *out) {
     const int jl = test_env_int("KH_NP_JLIM", 0);
     if (jl >= L1_THREADS * NP_KPT) N.jlim = std::min<uint32_t>(N.jlim, (uint32_t)jl);
     N.magic = (uint32_t)(((1ull << 32) + N.rp - 1) / N.rp);
-    for (uint64_t rho = 0; rho < Rm; rho++)
-        if ((uint32_t)((rho * N.magic) >> 32) != rho / N.rp) return false;
+    if (!np_magic_ok(Rm, N.rp, N.magic)) return false;
     N.pm = pm;
     N.ipm = 1.0 / (double)pm;
     *out = N;
     return true;
+}
+// the level-2 view of a three-level partition: fine buckets, fine records
+static NPGeo np_fine_geo(const NPGeo &C, const NPFine &Fi) {
+    NPGeo N = C;
+    N.rp = Fi.rp;
+    N.magic = Fi.magic;
+    N.nb = C.nb * Fi.F;
+    N.ob = Fi.ob;
+    N.pb = 32;
+    N.cap = Fi.cap;
+    N.rloc = Fi.rloc;
+    return N;
+}
+// fine bucket capacity (dense runs: the mean + the margin) and cursors;
+// returns the records of all fine buckets
+static uint64_t np_fine_plan(Graph *g, const NPGeo &C, NPFine &Fi, uint64_t nkmers) {
+    Workspace &w = g->ws;
+    const double mean = (double)nkmers * (double)((uint64_t)Fi.rp << C.s0) / (double)C.pm;
+    Fi.cap = ((uint64_t)(mean + g->cap_sigma * sqrt(mean)) + 64 + 1) & ~1ull;   // even: 16-B pair loads
+    const uint64_t nbf = (uint64_t)C.nb * Fi.F;
+    ensure((void **)&w.np_fcur, &w.cap_npfcur, nbf + 1, 8);
+    return Fi.cap * nbf;
 }
 // fixed-length 2-bit reads whose 4096-k-mer tile spans at most NP_TW packed words
 template <class Src>
@@ -995,7 +1056,8 @@ static bool complement_mode(const Graph *g, uint64_t nkmers, bool l2f) {
     if (g->ws.reg_max > (1ull << P.s0)) return false;
     if (force == 1) return true;
     const double p0 = (double)P.p[0], m = (double)nkmers;
-    const double z = std::max(0.0, p0 - (double)g->n_occupied);
+    const double occ = g->occ_hint >= 0 ? (double)g->occ_hint : (double)g->n_occupied;
+    const double z = std::max(0.0, p0 - occ);
     return z * (1.0 - std::exp(-m / p0)) > 0.6 * m;
 }
 
@@ -1206,10 +1268,12 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
     const bool l2f_try = l2f_wanted(g, nkmers);
     // near-prime partition: one level-1 record per k-mer (kh_nearprime.cuh)
     NPGeo npg{};
+    NPFine npf{};
     bool np = false;
     if constexpr (std::is_same<Src, SrcTwoBit>::value)
-        np = l2f_try && np_source(src) && l1f_chunk_tiles(g) >= 1 && np_geometry(g, &npg);
-    uint64_t cap2 = l2f_try ? reg_plan(g, nkmers, np) : 0;   // level-2 capacity (records)
+        np = l2f_try && np_source(src) && l1f_chunk_tiles(g) >= 1 && np_geometry(g, &npg, &npf);
+    const NPGeo np2 = npf.F ? np_fine_geo(npg, npf) : npg;   // the level-2 view (buckets, destinations)
+    uint64_t cap2 = l2f_try ? reg_plan(g, nkmers, np ? &np2 : nullptr) : 0;   // level-2 capacity (records)
     KH_HIP(hipMemsetAsync(w.ctr, 0, CTR_N * 8, st));
     if (bigc) {
         dev_fill(w.fullf, 0, flag_bytes, st);
@@ -1235,13 +1299,25 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
             if constexpr (std::is_same<Src, SrcTwoBit>::value) {
                 const uint32_t nwg = np_workgroups(g, nkmers, npg.nb);
                 const uint64_t capn = np_bkt_plan(g, npg, nkmers, nwg);
-                ensure_recs(g, std::max(capn, cap2));
+                // three levels: the fine records follow the coarse ones in rec1
+                const uint64_t fofs = (capn + 63) & ~63ull;
+                const uint64_t capf = npf.F ? np_fine_plan(g, npg, npf, nkmers) : 0;
+                ensure_recs(g, std::max(fofs + capf, cap2));
                 hipLaunchKernelGGL(k_np_reset, dim3(1), dim3(256), 0, st, w.np_cur, npg.nb, npg.cap);
                 KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, st));   // the chunk queue's head
                 TIMED("scatter_n1", hipLaunchKernelGGL(k_scatter_n1, dim3(nwg), dim3(L1_THREADS),
                                                        lds_n1((npg.nb + 3) & ~3u), st, npg, src, nkmers, w.np_cur,
                                                        w.rec1, w.np_blkj, w.ctr, l1f_blk_sh(), 0u,
                                                        np_chunk_tiles(g)));
+                if (npf.F) {
+                    const uint32_t nbf = npg.nb * npf.F;
+                    hipLaunchKernelGGL(k_np_reset, dim3((nbf + 255) / 256), dim3(256), 0, st, w.np_fcur, nbf,
+                                       npf.cap);
+                    const uint32_t pb = (uint32_t)std::max<uint64_t>(1, 4096 / npg.nb);
+                    TIMED("scatter_n1b", hipLaunchKernelGGL(k_scatter_n1b, dim3(npg.nb * pb), dim3(N1B_THREADS), 0, st,
+                                                            npg, npf, pb, w.np_cur, w.np_blkj, l1f_blk_sh(),
+                                                            w.rec1, w.np_fcur, w.rec1 + fofs, w.ctr));
+                }
             }
         } else if (ownf) {
             ensure_recs(g, std::max(cap1, cap2));
@@ -1344,7 +1420,15 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
             const bool bkt = l1f || ownf;   // level 1 went into fixed-capacity buckets
             const uint64_t *bs = bkt ? w.bkt_base : w.off1;
             const uint64_t *be = bkt ? w.bkt_cur : w.off1 + 1;
-            if (np) {
+            if (np && npf.F) {   // level 2 over the fine buckets of level 1b
+                const NPGeo fg = np_fine_geo(npg, npf);
+                const uint32_t nparts = l2f_parts(fg.nb);
+                const uint64_t fofs = (npg.cap * npg.nb + 63) & ~63ull;
+                TIMED("scatter_n2", hipLaunchKernelGGL(n2_kernel(fg.n), dim3(fg.nb * nparts), dim3(PT_THREADS),
+                                                       lds_scatter_n2(fg), st, fg, nparts, w.np_fcur, nullptr,
+                                                       l1f_blk_sh(), w.reg_base, (unsigned long long *)w.reg_cur,
+                                                       w.rec1 + fofs, w.rec2, w.ctr, l2f_blk_sh()));
+            } else if (np) {
                 const uint32_t nparts = l2f_parts(npg.nb);
                 TIMED("scatter_n2", hipLaunchKernelGGL(n2_kernel(npg.n), dim3(npg.nb * nparts), dim3(PT_THREADS),
                                                        lds_scatter_n2(npg), st, npg, nparts, w.np_cur, w.np_blkj,
@@ -1367,7 +1451,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
                 // exactly (histogram path), and the next 8 passes too
                 if (g->cap_sigma < 72.0 && recs_fit(g, nkmers, g->cap_sigma * 3.0)) {
                     g->cap_sigma *= 3.0;
-                    cap2 = reg_plan(g, nkmers, np);
+                    cap2 = reg_plan(g, nkmers, np ? &np2 : nullptr);
                     continue;
                 }
                 fast = false;
@@ -2147,7 +2231,7 @@ Graph::~Graph() {
     void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.fullf, w.newbits, w.bc, w.bcn, w.bck, w.bcv,
                     w.off1, w.ch2, w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.xseg, w.reg_base, w.reg_cur, w.bkt_base, w.bkt_cur, w.ctr, w.d_words, w.d_koff, w.d_bytes,
                     w.q_hashes, w.q_counts, w.frec, w.fcount, w.d_rbytes, w.sm_flags, w.sm_hash, w.cw_cur, w.cmbase,
-                    w.cnk, w.wch, w.np_cur, w.np_blkj};
+                    w.cnk, w.wch, w.np_cur, w.np_blkj, w.np_fcur};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (w.h_ctr) (void)hipHostFree(w.h_ctr);
@@ -2234,6 +2318,9 @@ struct ShardGroup {
         uint64_t cap_o8 = 0;         // sharded query: the reduced minima of this rank's k-mers
         uint8_t *dbuf = nullptr;
         uint64_t cap_dbuf = 0;       // delta mode: every rank's delta (then prefix) of the owned slices
+        // hosted delta mode: the alltoallv's host staging, kept across passes
+        // (about one table each way; only the slices' bytes are meaningful)
+        std::vector<uint8_t> hsend, hrecv;
         hipStream_t st_x = nullptr;
         hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
         bool freed[2] = {false, false};
@@ -2347,6 +2434,35 @@ static void group_make_shards(ShardGroup *G, int kind, int hash, int k, const ui
     const int world = G->world;
     const bool exchange = mode != 0;   // KH_GROUP_EXCHANGE or KH_GROUP_DELTA
     G->delta = mode == 2;
+    if (G->delta) {
+        // Delta mode keeps three table arenas a rank: the full-size view (its
+        // delta, then its prefix), the owner's delta buffer (about one table)
+        // and the rank's shard (1 / world of a table) -- it does not shard
+        // memory.  Fail before allocating when a device cannot hold its ranks'
+        // arenas (the record buffers of a pass come on top).
+        uint64_t tb = 0;
+        for (int i = 0; i < n; i++)
+            tb += kind == BIT ? sizes[i] / 8 + 1 : kind == NIBBLE ? sizes[i] / 2 + 1 : sizes[i];
+        const double per_rank = (double)tb * (2.0 + 1.0 / world);
+        for (int l = 0; l < G->nlocal; l++) {
+            int same = 0;
+            for (int m = 0; m < G->nlocal; m++) same += devices[m] == devices[l];
+            size_t freeb = 0, total = 0;
+            KH_HIP(hipSetDevice(devices[l]));
+            if (hipMemGetInfo(&freeb, &total) != hipSuccess) {
+                (void)hipGetLastError();
+                continue;
+            }
+            if (per_rank * same > 0.95 * (double)freeb) {
+                char msg[256];
+                snprintf(msg, sizeof msg,
+                         "delta mode needs %.1f GB of table arenas per rank (%d on device %d, %.1f GB free); "
+                         "exchange mode shards the tables (--group-mode exchange)",
+                         per_rank / 1e9, same, devices[l], (double)freeb / 1e9);
+                fail(KH_EVALUE, msg);
+            }
+        }
+    }
     if (exchange) {
         // exchange-mode views hold only a geometry and a workspace; delta-mode
         // views also a full-size table arena (the rank's delta, then its prefix)
@@ -3306,7 +3422,8 @@ static void delta_exchange(ShardGroup *G, bool forward) {
             rb[d] = forward ? stride[r] : stride[d];
             at[d + 1] = at[d] + sb[d];
         }
-        std::vector<uint8_t> hs(at[W] + 1), hr;
+        std::vector<uint8_t> &hs = lc.hsend, &hr = lc.hrecv;
+        if (hs.size() < at[W] + 1) hs.resize(at[W] + 1);
         KH_HIP(hipStreamSynchronize(st));
         for (int d = 0; d < W; d++)
             for (int i = 0; i < n; i++) {
@@ -3323,7 +3440,7 @@ static void delta_exchange(ShardGroup *G, bool forward) {
             }
         uint64_t rtot = 0;
         for (int d = 0; d < W; d++) rtot += rb[d];
-        hr.resize(rtot + 1);
+        if (hr.size() < rtot + 1) hr.resize(rtot + 1);
         host_rc(G->tp.alltoallv(G->tp.ctx, hs.data(), sb.data(), hr.data(), rb.data()), "alltoallv");
         uint64_t q = 0;
         for (int s = 0; s < W; s++) {
@@ -3427,6 +3544,11 @@ static void group_consume_delta(ShardGroup *G, const GroupReads &R) {
             V->profile = sh->profile;
             srcs[l] = group_src<Src>(V, R, R.d[l], r0, nr);
             bool f = false;
+            // complement mode's winner-share estimate: the table's occupancy,
+            // scaled up from the home shard's slice of table 0 (the view's own
+            // counters stay 0: a2a_stage_c counts into the home shard)
+            const Params &SP = sh->prm;
+            V->occ_hint = SP.lsz[0] ? (int64_t)((double)sh->n_occupied * (double)SP.p[0] / (double)SP.lsz[0]) : -1;
             ps[l] = pass_stage_a(V, srcs[l], nkc, false, &f);
             fast[l] = f;
             delta_apply(V, ps[l], f);

@@ -148,12 +148,16 @@ struct Workspace {
     uint64_t *reg_base = nullptr;    // [regions + 1] capacity prefix for passes of reg_nkmers k-mers
     uint64_t *reg_cur = nullptr;     // [regions] append cursors
     uint64_t cap_reg = 0, reg_nkmers = 0, reg_total = 0, reg_max = 0;   // reg_max: largest region capacity
-    bool reg_np = false;             // planned for the near-prime level 2 (two writing buckets a region)
+    uint64_t reg_np = 0;             // planned for the near-prime level 2: its rp, rloc, parts (0: not)
     // near-prime level 1 (kh_nearprime.cuh): bucket d holds [d cap, np_cur[d]);
     // np_blkj[block] = the k-mer index base of a level-1 block
     unsigned long long *np_cur = nullptr;
     uint32_t *np_blkj = nullptr;
     uint64_t cap_npcur = 0, cap_blkj = 0;
+    // three-level near-prime: fine bucket b holds [b cap_f, np_fcur[b]) of
+    // the fine records (kh_nearprime.cuh k_scatter_n1b)
+    unsigned long long *np_fcur = nullptr;
+    uint64_t cap_npfcur = 0;
     double reg_sigma = 0, bkt_sigma = 0;          // capacity margins the plans were made with
     // fixed-capacity level 1 (k_scatter_l1f): bucket b holds [bkt_base[b], bkt_cur[b])
     uint64_t *bkt_base = nullptr, *bkt_cur = nullptr;
@@ -259,6 +263,7 @@ struct Graph {
     uint64_t arena_bytes = 0;
     hipStream_t stream = nullptr;
     uint64_t n_unique = 0, n_occupied = 0;
+    int64_t occ_hint = -1;            // delta-mode views: the table occupancy complement_mode estimates from (-1: n_occupied)
     bool use_bigcount = false;
     std::unordered_map<uint64_t, uint16_t> bigcounts;   // storage.hh:498 KmerCountMap
     // device mirror of bigcounts for queries (sorted keys / values)

@@ -381,7 +381,7 @@ __global__ void __launch_bounds__(THREADS) k_scatter_n2(NPGeo N, uint32_t parts,
             uint32_t y = 0;
             if (idx < n1) {
                 x = *(const ulonglong2 *)(rec_in + idx);
-                y = blkj[idx >> blk_sh1];
+                y = blkj ? blkj[idx >> blk_sh1] : 0u;   // none: fine records of level 1b (pb = 32)
             }
             v[2 * q] = x.x;
             v[2 * q + 1] = idx + 1 < n1 ? x.y : ~0ull;
@@ -533,6 +533,115 @@ using N2Fn = void (*)(NPGeo, uint32_t, const unsigned long long *, const uint32_
                       unsigned long long *, const uint64_t *, uint64_t *, uint64_t *, int);
 static N2Fn n2_kernel(int n) {
     return n == 2 ? k_scatter_n2<PT_THREADS, 2> : n == 3 ? k_scatter_n2<PT_THREADS, 3> : k_scatter_n2<PT_THREADS, 4>;
+}
+
+// ---------------------------------------------------------------------------
+// Level 1b (three levels: tables too large for <= 256 level-1 buckets of the
+// level-2 fan-out, C4's 4 x 8e9): level 1 buckets each k-mer by r into coarse
+// buckets of F x R' regions (k_scatter_n1 as above, <= 256 of them), and this
+// kernel splits every coarse bucket into its F fine buckets of R' regions,
+// still one record per k-mer:
+//     fine record = j << 32 | q << ob_f | (r - fine bucket's first bin)
+// (absolute pass index j: a fine bucket gathers records of many level-1
+// blocks).  A workgroup streams a slice of one coarse bucket in tiles of
+// THREADS x 8 records: LDS rank per fine bucket, one returning atomic per
+// (tile, fine bucket) reserves a dense run, the tile is staged in LDS in run
+// order and written out coalesced.  No blocks, pads or sentinels in the
+// output; k_scatter_n2 reads it with pb = 32 and no block bases.
+struct NPFine {
+    uint32_t F;        // fine buckets per coarse bucket (0: two levels)
+    uint32_t rp;       // regions of 2^s0 bins per fine bucket
+    uint32_t magic;    // ceil(2^32 / rp)
+    int ob;            // offset bits of a fine record
+    uint32_t rloc;     // level-2 destinations per table of a fine bucket (rp + spill)
+    uint64_t cap;      // records per fine bucket (fine bucket b owns [b cap, (b + 1) cap))
+};
+constexpr int N1B_THREADS = 256;
+constexpr int N1B_IN = 8;          // records per thread a tile
+constexpr uint32_t N1B_MAXF = 16;
+__global__ void __launch_bounds__(N1B_THREADS) k_scatter_n1b(NPGeo C, NPFine Fi, uint32_t parts,
+                                                              const unsigned long long *bkt_end, const uint32_t *blkj,
+                                                              int blk_sh1, const uint64_t *rec_in,
+                                                              unsigned long long *fcur, uint64_t *rec_out,
+                                                              uint64_t *ctr) {
+    constexpr int TILE = N1B_THREADS * N1B_IN;
+    __shared__ __attribute__((aligned(16))) uint64_t slot[TILE];
+    __shared__ uint8_t sf[TILE];
+    __shared__ uint32_t hist[N1B_MAXF], lstart[N1B_MAXF + 1];
+    __shared__ uint64_t gbase[N1B_MAXF];
+    if (__builtin_amdgcn_readfirstlane((uint32_t)ctr[CTR_ERR]) & 8u) return;
+    const uint32_t c = blockIdx.x / parts, p = blockIdx.x % parts;
+    const uint64_t b0 = (uint64_t)c * C.cap, b1 = min((uint64_t)bkt_end[c], b0 + C.cap);
+    const uint64_t len = ((b1 - b0 + parts - 1) / parts + 1) & ~1ull;
+    const uint64_t r0 = min(b1, b0 + (uint64_t)p * len), r1 = min(b1, r0 + len);
+    const uint64_t pmask = (1ull << C.pb) - 1, omask = (1ull << C.ob) - 1;
+    const uint64_t Sf = (uint64_t)Fi.rp << C.s0;   // bins of a fine bucket
+    const uint32_t F = Fi.F;
+    for (uint64_t t0 = r0; t0 < r1; t0 += TILE) {
+        if (threadIdx.x < N1B_MAXF) hist[threadIdx.x] = 0;
+        block_sync();
+        uint64_t v[N1B_IN];
+        uint32_t rk[N1B_IN];
+#pragma unroll
+        for (int q = 0; q < N1B_IN / 2; q++) {
+            const uint64_t idx = t0 + 2 * ((uint64_t)q * N1B_THREADS + threadIdx.x);
+            ulonglong2 x = make_ulonglong2(~0ull, ~0ull);
+            uint32_t jb = 0;
+            if (idx < r1) {
+                x = *(const ulonglong2 *)(rec_in + idx);
+                jb = blkj[idx >> blk_sh1];
+                if (idx + 1 >= r1) x.y = ~0ull;
+            }
+            v[2 * q] = x.x;
+            v[2 * q + 1] = x.y;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                uint64_t &y = v[2 * q + h];
+                if (y == ~0ull) continue;
+                const uint64_t j = (uint32_t)(jb + (uint32_t)(y >> C.pb));
+                const uint64_t pay = y & pmask;
+                const uint64_t off = pay & omask;
+                const uint32_t f = __umulhi((uint32_t)(off >> C.s0), Fi.magic);
+                y = (j << 32) | ((pay >> C.ob) << Fi.ob) | (off - (uint64_t)f * Sf);
+                rk[2 * q + h] = (f << 24) | atomicAdd(&hist[f], 1u);
+            }
+        }
+        block_sync();
+        if (threadIdx.x < F) {
+            const uint32_t f = threadIdx.x, h = hist[f];
+            const uint64_t fb = (uint64_t)c * F + f;
+            uint64_t gb = h ? atomicAdd(&fcur[fb], (unsigned long long)h) : 0;
+            if (h && gb + h > (fb + 1) * Fi.cap) {
+                atomicOr((unsigned long long *)&ctr[CTR_ERR], 8ull);
+                gb = ~0ull;
+            }
+            gbase[f] = gb;
+        }
+        if (threadIdx.x == 0) {
+            uint32_t a = 0;
+            for (uint32_t f = 0; f < F; f++) {
+                lstart[f] = a;
+                a += hist[f];
+            }
+            lstart[F] = a;
+        }
+        block_sync();
+#pragma unroll
+        for (int a = 0; a < N1B_IN; a++) {
+            if (v[a] == ~0ull) continue;
+            const uint32_t f = rk[a] >> 24;
+            const uint32_t s = lstart[f] + (rk[a] & 0xFFFFFFu);
+            slot[s] = v[a];
+            sf[s] = (uint8_t)f;
+        }
+        block_sync();
+        const uint32_t nv = lstart[F];
+        for (uint32_t m = threadIdx.x; m < nv; m += N1B_THREADS) {
+            const uint32_t f = sf[m];
+            const uint64_t gb = gbase[f];
+            if (gb != ~0ull) rec_out[gb + (m - lstart[f])] = slot[m];
+        }
+    }
 }
 
 // level-1 bucket cursors start at d * cap

@@ -98,7 +98,8 @@ def make_snapshots(names):
         while marks and marks[0][0] == r0:
             _, n = marks.pop(0)
             _write(n, FD.CONFIGS[n], t, sizes, kmers, time.time() - t0,
-                   ", snapshot at read %d of a %d-read pass" % (r0, last))
+                   ", snapshot at read %d of a %d-read pass%s" % (r0, last, ", %d hash threads" % THREADS
+                                                                  if THREADS > 1 else ""))
 
 
 if __name__ == "__main__":

@@ -12,7 +12,10 @@ regions past a bucket's range) and k = 21 at C2's own 4 x ~1e9 (255 buckets,
 index span a level-1 block may hold, so nearly every block is closed early
 with sentinels; KH_NEAR_PRIME=0 runs the per-table level 1 on the same
 stream, and the skewed genomic stream overflows the fixed capacities and
-takes the fallback."""
+takes the fallback.  KH_NP_L1MAX caps the level-1 buckets, so these tables
+take the three-level partition C4's 4 x 8e9 takes (k_scatter_n1b splits
+each coarse bucket into up to 16 fine buckets, fine records j << 32 |
+q << ob | offset)."""
 import ctypes
 import os
 
@@ -80,7 +83,7 @@ def _kernels(g):
     return {ln.split("\t")[0] for ln in buf.value.decode().splitlines() if ln}
 
 
-@pytest.mark.parametrize("mode", ["near_prime", "closing_blocks", "per_table"])
+@pytest.mark.parametrize("mode", ["near_prime", "closing_blocks", "per_table", "three_level"])
 def test_nearprime_matches_oracle(stream, mode, monkeypatch):
     import khmer_amd
     from khmer_amd._lib import lib, check
@@ -88,6 +91,10 @@ def test_nearprime_matches_oracle(stream, mode, monkeypatch):
         monkeypatch.setenv("KH_NP_JLIM", "8191")   # blocks span at most ~2 tiles
     if mode == "per_table":
         monkeypatch.setenv("KH_NEAR_PRIME", "0")
+    if mode == "three_level":
+        # k = 19, 1e8: 8 coarse buckets of 13 fine ones (63 regions each);
+        # C2's geometry: 124 coarse buckets of 16 fine ones (31 regions each)
+        monkeypatch.setenv("KH_NP_L1MAX", "8" if stream["k"] == 19 else "128")
     g = khmer_amd.Countgraph(stream["k"], stream["x"], stream["tables"])
     g.set_use_bigcount(True)
     check(lib.kh_graph_set_batch_kmers(g._g, stream["batch"]))   # several device passes
@@ -101,6 +108,7 @@ def test_nearprime_matches_oracle(stream, mode, monkeypatch):
         # the near-prime path ran (the skewed genomic stream may overflow the
         # fixed capacities and fall back; its tables must still be exact)
         assert {"scatter_n1", "scatter_n2", "apply_byte"} <= kernels, kernels
+        assert ("scatter_n1b" in kernels) == (mode == "three_level"), kernels
     want = stream["want"]
     tabs = g.get_raw_tables()
     for i in range(stream["tables"]):
