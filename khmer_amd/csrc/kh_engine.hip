@@ -1303,6 +1303,7 @@ static PassState pass_stage_a(Graph *g, const Src &src, uint64_t nkmers, bool ap
                 const uint64_t fofs = (capn + 63) & ~63ull;
                 const uint64_t capf = npf.F ? np_fine_plan(g, npg, npf, nkmers) : 0;
                 ensure_recs(g, std::max(fofs + capf, cap2));
+                if (KH_ABL(P, 16)) dev_fill(w.rec1, 0xFF, capn * 8, st);   // timing only: level 2 sees sentinels
                 hipLaunchKernelGGL(k_np_reset, dim3(1), dim3(256), 0, st, w.np_cur, npg.nb, npg.cap);
                 KH_HIP(hipMemsetAsync(w.ctr + CTR_L1Q, 0, 8, st));   // the chunk queue's head
                 TIMED("scatter_n1", hipLaunchKernelGGL(k_scatter_n1, dim3(nwg), dim3(L1_THREADS),
