@@ -12,7 +12,9 @@ finalize), i.e. the whole hot path over the whole batch.
 Multi-GPU (one rank per GPU; `--gpus N` starts the N rank processes itself
 unless a launcher set WORLD_SIZE): every table is split into G contiguous bin
 ranges, one per rank.  Every rank generates its own 50M
-reads (weak scaling).  Default group mode "delta": every rank counts its own
+reads (weak scaling).  Group mode "auto" (the default) picks delta unless the
+tables outweigh the records a rank-pass sends (auto_group_mode: C4 strong
+scaling takes exchange).  Delta mode: every rank counts its own
 reads into full-size delta tables, the owners turn every rank's deltas of
 their slice into per-rank prefixes (table bytes over RCCL/xGMI, grouped
 send/recv) and each rank re-applies its reads over its prefix; "exchange"
@@ -85,8 +87,9 @@ def parse():
                          "0 = iid uniform reads")
     ap.add_argument("--strong", action="store_true",
                     help="multi-GPU strong scaling: --reads is the whole job, split over the ranks")
-    ap.add_argument("--group-mode", choices=["delta", "exchange", "broadcast"], default="delta",
-                    help="multi-GPU: 'delta' (default: every rank counts its own reads into full-size delta tables, "
+    ap.add_argument("--group-mode", choices=["auto", "delta", "exchange", "broadcast"], default="auto",
+                    help="multi-GPU: 'auto' (default: delta unless the tables outweigh the records a rank-pass "
+                         "would send, DESIGN.md §6), 'delta' (every rank counts its own reads into full-size delta tables, "
                          "owners turn every rank's deltas of their slice into per-rank prefixes, each rank applies "
                          "its reads over its prefix; only table bytes travel), 'exchange' (Option A: every rank "
                          "hashes only its own reads and sends each level-1 bucket to its owner) or 'broadcast' "
@@ -111,8 +114,24 @@ def parse():
     a.bigcount = a.graph == "Countgraph" and not a.no_bigcount
     a.genome = int(a.genome)
     a.murmur = a.graph in MURMUR
+    if a.group_mode == "auto":
+        a.group_mode = auto_group_mode(a)
     a.exchange = a.group_mode == "exchange"
     return a
+
+
+def auto_group_mode(a):
+    """Delta or exchange for this run.  Per rank-pass, delta
+    mode sends the table bytes TB twice (deltas to the owners, prefixes back),
+    exchange mode every (k-mer, table) record once (8 B x tables per k-mer):
+    delta iff TB <= 4 x tables x the k-mers of a rank-pass.  C2 / C4 weak
+    scaling (3.25e9 k-mers a rank-pass): delta; C4 strong over 8 ranks (0.8e9
+    k-mers a rank, 32 GB of tables): exchange."""
+    bytes_per_bin = {"Countgraph": 1.0, "Nodegraph": 0.125, "SmallCountgraph": 0.5, "SmallCounttable": 0.5}[a.graph]
+    tb = a.tables * a.x * bytes_per_bin
+    reads = (a.reads + a.gpus - 1) // a.gpus if (a.strong and a.gpus > 1) else a.reads
+    kpass = min(a.batch_kmers, reads * (a.read_len - a.k + 1))
+    return "delta" if tb <= 4.0 * a.tables * kpass else "exchange"
 
 
 FIXTURE_GRAPH = {(1, 0): "Countgraph", (2, 0): "Nodegraph", (7, 0): "SmallCountgraph", (7, 1): "SmallCounttable"}

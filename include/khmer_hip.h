@@ -323,6 +323,11 @@ int kh_group_mode(kh_group *grp, int *mode);
 /* bins [lo, lo + size) of table `table` held by rank `rank` (any rank) */
 int kh_group_rank_slice(kh_group *grp, int rank, int table, uint64_t *lo, uint64_t *size);
 int kh_group_counters(kh_group *grp, uint64_t *n_unique, uint64_t *n_occupied);   /* collective */
+/* delta mode: bytes of the table pieces this process's ranks exchanged with
+ * other ranks so far, as dense slices and as sent (sparse pieces: a bitmap of
+ * the nonzero bytes plus those bytes; KH_DELTA_SPARSE=0 sends them dense).
+ * No reference counterpart: the wire accounting of the MI355X group modes. */
+int kh_group_wire_stats(kh_group *grp, uint64_t *dense_bytes, uint64_t *sent_bytes);
 /* The Counttable family (MurmurHash3) in a group: the same
  * collective consume over ASCII fixed-length reads (d_bytes[l] = local shard
  * l's own reads; hash_kind KH_HASH_MURMUR at group creation).  Replaces the

@@ -68,6 +68,7 @@ SIGNATURES = {
     "kh_group_slice": (i32, [P, i32, i32, PU64, PU64]),
     "kh_group_consume_packed_fixed_device": (i32, [P, ctypes.POINTER(P), u64, u64]),
     "kh_group_counters": (i32, [P, PU64, PU64]),
+    "kh_group_wire_stats": (i32, [P, PU64, PU64]),
     "kh_group_consume_bytes_fixed_device": (i32, [P, ctypes.POINTER(P), u64, u64]),
     "kh_group_median_fixed_device": (i32, [P, ctypes.POINTER(P), u64, u64, ctypes.POINTER(P), ctypes.POINTER(P),
                                            ctypes.POINTER(P)]),

@@ -581,6 +581,231 @@ __global__ void __launch_bounds__(TH, 4) k_apply_count(Params P, ApplyArgs A) {
     if ((threadIdx.x & 63) == 0 && occ) atomicAdd((unsigned long long *)&A.ctr[CTR_OCC], (unsigned long long)occ);
 }
 
+// Record-driven apply for sparse regions (C4 / C5 / C5M: ~6-7K records over
+// 2^14 bins; the host takes it when every region's capacity fits the
+// APPLY_RECS x 1024 records the workgroup prefetches, so a region's records
+// ARE the registers the prefetch filled).  The same batch semantics as
+// k_apply_count's coarse path (ByteStorage::add / NibbleStorage::add,
+// storage.hh:571-624 / 320-359), but nothing walks the 2^14 bins:
+//  - cnt / minj are zero / NO_J between regions: each region resets the bins
+//    its records touched (and the staging slots it used) instead of clearing
+//    128 KB of LDS;
+//  - pass 1 runs per record: the record whose k-mer index is its bin's
+//    minimum owns the bin (one record per (k-mer, region): a region is one
+//    table) and computes the bin's saturated value, winner (bin zero before
+//    the pass), crossing and changed chunk; every record knows whether it is
+//    listed (a winner, or in complement mode a loser) and whether its bin was
+//    full before the batch (bigcount: full_add directly, no full255 re-read);
+//  - the listed k-mer indices go from registers into the coarse-window runs.
+// Barriers a region: table chunk + state in, count atomics, per-record reads,
+// owner writes + resets, write-back + runs, reset of the staging slots.
+template <int KIND, bool LOS>
+__global__ void __launch_bounds__(1024, 1) k_apply_sparse(Params P, ApplyArgs A) {
+    constexpr int TH = 1024;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t R = 1u << P.s0;
+    uint32_t *cnt = (uint32_t *)smem;      // [R] zero between regions; the runs' staging array
+    uint32_t *minj = cnt + R;              // [R] NO_J between regions
+    uint8_t *c0 = (uint8_t *)(minj + R);   // [R] the region's values
+    uint32_t *chg = (uint32_t *)(c0 + R);  // [R/512] changed 16-bin chunks
+    uint32_t *s_flag = chg + R / 512;      // [4] [1] crossings
+    uint32_t *chist = s_flag + 4;          // [MAX_CW] window counts
+    uint32_t *cst0 = chist + MAX_CW;       // [MAX_CW] window's first staging slot
+    uint32_t *ccur = cst0 + MAX_CW;        // [MAX_CW] placement cursors
+    uint32_t *s_q = ccur + MAX_CW;         // [2] region queue
+    unsigned long long *cgb = (unsigned long long *)(s_q + 2);   // [MAX_CW] output bases
+    const uint32_t MAXC = KIND == BYTE ? 255u : 15u;
+    const bool bigc = KIND == BYTE && P.use_bigcount;
+    const uint32_t t = threadIdx.x;
+    const int cjs = A.cjs;
+    uint64_t occ = 0;
+    const uint64_t total = A.rprefix[P.n];
+    for (uint32_t x = t; x < R / 4; x += TH) {
+        ((uint4 *)cnt)[x] = make_uint4(0, 0, 0, 0);
+        ((uint4 *)minj)[x] = make_uint4(NO_J, NO_J, NO_J, NO_J);
+    }
+    Prefetch cur, nxt;
+    const uint64_t G = gridDim.x;
+    uint64_t r1 = blockIdx.x + G, r2 = blockIdx.x + 2 * G;
+    uint32_t par = 0;
+    prefetch_region<KIND, TH>(P, A, blockIdx.x, total, load_bounds(P, A, blockIdx.x, total), cur);
+    Bounds bnext = load_bounds(P, A, r1, total);
+    for (uint64_t rr = blockIdx.x; rr < total;) {
+        unsigned long long qn = 0;
+        if (A.dyn && t == 0) qn = atomicAdd((unsigned long long *)&A.ctr[CTR_APQ], 1ull);
+        auto publish = [&]() {
+            if (A.dyn && t == 0) s_q[par] = (uint32_t)min<unsigned long long>(qn + 3 * G, total);
+        };
+        auto advance = [&]() {
+            rr = r1;
+            r1 = r2;
+            r2 = A.dyn ? (uint64_t)uniform_u32(s_q[par]) : r2 + G;
+            par ^= 1;
+        };
+        const RegionInfo ri = cur.ri;
+        if (ri.e0 == ri.e1) {
+            if (t == 0) A.wcnt[rr] = 0;
+            prefetch_region<KIND, TH>(P, A, r1, total, bnext, cur);
+            bnext = load_bounds(P, A, r2, total);
+            if (A.dyn) {
+                block_sync();
+                publish();
+                block_sync();
+            }
+            advance();
+            continue;
+        }
+        const Bounds bafter = load_bounds(P, A, r2, total);
+        const uint32_t nb = ri.nb;
+        const uint32_t nchunk = (nb + 15) / 16;
+        uint8_t *tab = A.tab + P.tbyte[ri.i];
+        if (t < nchunk) {
+            if (KIND == BYTE) {
+                ((uint4 *)c0)[t] = cur.tv;
+            } else {
+                uint4 o;
+                uint32_t *ow = (uint32_t *)&o;
+                const uint32_t w[2] = {cur.tv.x, cur.tv.y};
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+#pragma unroll
+                    for (int b2 = 0; b2 < 2; b2++) {
+                        const uint32_t x = (w[h] >> (16 * b2)) & 0xFFFFu;   // 2 bytes = 4 bins
+                        const uint32_t lo = x & 0xFF, hi = x >> 8;
+                        ow[2 * h + b2] = (lo >> 4) | ((lo & 15) << 8) | ((hi >> 4) << 16) | ((hi & 15) << 24);
+                    }
+                }
+                ((uint4 *)c0)[t] = o;
+            }
+        }
+        if (t < R / 512) chg[t] = 0;
+        if (t < MAX_CW) chist[t] = ccur[t] = 0;
+        if (t == 0) s_flag[1] = 0;
+        block_sync();
+#pragma unroll
+        for (int u = 0; u < APPLY_RECS; u++) count_record(cur.v[u], cnt, minj);
+        block_sync();
+        // per record: owner of its bin?  listed?  (reads only: the owners'
+        // writes wait for the barrier below)
+        uint32_t lst = 0, own = 0;
+        uint32_t fv[APPLY_RECS];
+#pragma unroll
+        for (int u = 0; u < APPLY_RECS; u++) {
+            fv[u] = 0;
+            const uint64_t x = cur.v[u];
+            if (x == ~0ull) continue;
+            const uint32_t o = (uint32_t)x, j = (uint32_t)(x >> 32);
+            const uint32_t c = c0[o];
+            const bool ow = minj[o] == j;
+            const bool win = ow && c == 0;
+            if (bigc && c == 255) full_add(A.fullf, j);   // every insert into a bin full before the batch
+            if (LOS ? !win : win) {
+                lst |= 1u << u;
+                atomicAdd(&chist[j >> cjs], 1u);
+            }
+            if (ow) {
+                const uint32_t v = c + cnt[o];
+                const uint32_t f = v < MAXC ? v : MAXC;
+                if (bigc && c < 255 && v > 255) {   // insert r sees c + r: full iff c + r >= 255, r < n
+                    const uint32_t idx = atomicAdd(&s_flag[1], 1u);
+                    A.xent[ri.e0 + idx] = (o << 8) | c;
+                }
+                if (f != c) {
+                    own |= 1u << u;
+                    fv[u] = f;
+                }
+                occ += ri.i == 0 && win;
+            }
+        }
+        block_sync();
+        // owners write their bins' values; every record resets its bin
+#pragma unroll
+        for (int u = 0; u < APPLY_RECS; u++) {
+            const uint64_t x = cur.v[u];
+            if (x == ~0ull) continue;
+            const uint32_t o = (uint32_t)x;
+            if ((own >> u) & 1u) {
+                c0[o] = (uint8_t)fv[u];
+                atomicOr(&chg[o >> 9], 1u << ((o >> 4) & 31));
+            }
+            cnt[o] = 0;
+            minj[o] = NO_J;
+        }
+        publish();
+        if (bigc && t == 0 && s_flag[1]) {
+            const uint64_t seg = atomicAdd((unsigned long long *)&A.ctr[CTR_NCROSS], 1ull);
+            A.xseg[seg] = make_uint4((uint32_t)ri.e0, (uint32_t)(ri.e0 >> 32), (uint32_t)(ri.e1 - ri.e0), s_flag[1]);
+        }
+        // window bases: every wave scans the window counts itself (lane c:
+        // window c); wave 0 reserves the runs
+        const uint32_t lane = t & 63;
+        const uint32_t cc = chist[lane];
+        uint32_t incl = cc;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= (uint32_t)d) incl += y;
+        }
+        const uint32_t st0 = incl - cc;
+        const uint32_t wall = __shfl(incl, 63, 64);
+        unsigned long long my_gb = 0;
+        if (t < 64 && cc) my_gb = atomicAdd(&A.cw_cur[t], (unsigned long long)cc);
+        prefetch_region<KIND, TH>(P, A, r1, total, bnext, nxt);
+        bnext = bafter;
+        block_sync();
+        // changed 16-bin chunks back to the table
+        for (uint32_t x = t; x < nchunk; x += TH) {
+            if (!((chg[x >> 5] >> (x & 31)) & 1)) continue;
+            const uint4 cv = ((const uint4 *)c0)[x];
+            if (KIND == BYTE) {
+                ((uint4 *)(tab + ri.bin_lo))[x] = cv;
+            } else {
+                // even bin -> high nibble (storage.hh:262-272)
+                const uint8_t *fin = (const uint8_t *)&cv;
+                uint2 o;
+                uint32_t *ow = (uint32_t *)&o;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        w |= (uint32_t)((fin[8 * h + 2 * b] << 4) | fin[8 * h + 2 * b + 1]) << (8 * b);
+                    ow[h] = w;
+                }
+                ((uint2 *)(tab + (ri.bin_lo >> 1)))[x] = o;
+            }
+        }
+        // listed k-mer indices -> staging (the reset count array) by window
+#pragma unroll
+        for (int u = 0; u < APPLY_RECS; u++) {
+            if (!__ballot((lst >> u) & 1u)) continue;   // wave-uniform: the shuffle needs every lane
+            const bool ok = (lst >> u) & 1u;
+            const uint32_t j = (uint32_t)(cur.v[u] >> 32);
+            const uint32_t c = ok ? j >> cjs : 0u;
+            const uint32_t base = __shfl(st0, (int)c, 64);
+            if (ok) cnt[base + atomicAdd(&ccur[c], 1u)] = j;
+        }
+        if (t == 0) A.wcnt[rr] = wall;
+        if (t < 64) {
+            cgb[t] = my_gb;
+            cst0[t] = st0;
+        }
+        block_sync();
+        for (uint32_t x = t; x < wall; x += TH) {
+            const uint32_t v = cnt[x], c = v >> cjs;
+            A.wco[cgb[c] + (x - cst0[c])] = v;
+        }
+        block_sync();
+        for (uint32_t x = t; x < wall; x += TH) cnt[x] = 0;   // ordered before the next count atomics by its first barrier
+        cur = nxt;
+        advance();
+    }
+    occ = wave_sum(occ);
+    if ((threadIdx.x & 63) == 0 && occ) atomicAdd((unsigned long long *)&A.ctr[CTR_OCC], (unsigned long long)occ);
+}
+__host__ __device__ constexpr size_t lds_apply_sparse(size_t R) {
+    return R * 4 * 2 + (R / 512) * 4 + 16 + MAX_CW * 4 * 3 + 8 + MAX_CW * 8 + R;
+}
+
 // Bit storage (Bloom): BitStorage::test_and_set_bits (storage.hh:172-199)
 // TH threads over a region of 2^14 bins (BPT bins per thread).  Coarse-window
 // winners (A.coarse) are counting-sorted in LDS exactly as in k_apply_count,
@@ -1502,6 +1727,107 @@ __global__ void k_delta_prefix(uint8_t *T, uint8_t *buf, uint64_t nbytes, uint64
                 T[x] = (uint8_t)tv;
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Sparse delta pieces (delta mode's table exchange, kh_engine.hip
+// delta_exchange): a byte range of nb bytes travels as a bitmap of its
+// nonzero bytes (a u16 mask per 16 bytes, nb / 8 bytes) followed by the
+// nonzero bytes in order.  A workgroup of 256 threads codes one 4096-byte
+// chunk (16 bytes a thread); chunk payload offsets come from an exclusive
+// scan of the per-chunk counts (sender: from the bytes, receiver: from the
+// bitmap).  The ranges are 16-byte aligned (the host checks).
+constexpr uint32_t SP_CHUNK = 4096;
+constexpr int SP_THREADS = 256;
+__device__ __forceinline__ uint32_t sp_mask16(uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) m |= (((w[q] >> (8 * b)) & 0xFFu) != 0u ? 1u : 0u) << (4 * q + b);
+    return m;
+}
+// this thread's 16 bytes (zero past nb)
+__device__ __forceinline__ uint4 sp_load16(const uint8_t *src, uint64_t x0, uint64_t nb) {
+    if (x0 + 16 <= nb) return *(const uint4 *)(src + x0);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    uint8_t *b = (uint8_t *)&v;
+    for (uint64_t x = x0; x < nb; x++) b[x - x0] = src[x];
+    return v;
+}
+// block-wide exclusive prefix of n (256 threads), total in *tot
+__device__ __forceinline__ uint32_t sp_block_prefix(uint32_t n, uint32_t *s_w, uint32_t *tot) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t incl = n;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+    }
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+    for (uint32_t q = 0; q < SP_THREADS / 64; q++) {
+        before += q < wv ? s_w[q] : 0u;
+        all += s_w[q];
+    }
+    *tot = all;
+    return before + incl - n;
+}
+// per-chunk nonzero counts, from the bytes (bm == null) or from the bitmap;
+// cnt[nchunks] = 0 (the scan's last value is then the total)
+__global__ void __launch_bounds__(SP_THREADS) k_sp_count(const uint8_t *src, const uint16_t *bm, uint64_t nb,
+                                                         uint32_t *cnt) {
+    __shared__ uint32_t s_w[SP_THREADS / 64];
+    const uint64_t c = blockIdx.x;
+    const uint64_t x0 = c * SP_CHUNK + 16ull * threadIdx.x;
+    uint32_t n = 0;
+    if (x0 < nb) n = __popc(bm ? (uint32_t)bm[x0 / 16] : sp_mask16(sp_load16(src, x0, nb)));
+    uint32_t tot;
+    (void)sp_block_prefix(n, s_w, &tot);
+    if (threadIdx.x == 0) {
+        cnt[c] = tot;
+        if (c + 1 == gridDim.x) cnt[c + 1] = 0;
+    }
+}
+__global__ void __launch_bounds__(SP_THREADS) k_sp_pack(const uint8_t *src, uint64_t nb, const uint64_t *off,
+                                                        uint16_t *bm, uint8_t *pay) {
+    __shared__ uint32_t s_w[SP_THREADS / 64];
+    const uint64_t c = blockIdx.x;
+    const uint64_t x0 = c * SP_CHUNK + 16ull * threadIdx.x;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    uint32_t m = 0;
+    if (x0 < nb) {
+        v = sp_load16(src, x0, nb);
+        m = sp_mask16(v);
+        bm[x0 / 16] = (uint16_t)m;
+    }
+    uint32_t tot;
+    uint64_t pos = off[c] + sp_block_prefix((uint32_t)__popc(m), s_w, &tot);
+    const uint8_t *b = (const uint8_t *)&v;
+#pragma unroll
+    for (int q = 0; q < 16; q++)
+        if ((m >> q) & 1u) pay[pos++] = b[q];
+}
+__global__ void __launch_bounds__(SP_THREADS) k_sp_unpack(const uint16_t *bm, const uint8_t *pay, const uint64_t *off,
+                                                          uint64_t nb, uint8_t *dst) {
+    __shared__ uint32_t s_w[SP_THREADS / 64];
+    const uint64_t c = blockIdx.x;
+    const uint64_t x0 = c * SP_CHUNK + 16ull * threadIdx.x;
+    const uint32_t m = x0 < nb ? (uint32_t)bm[x0 / 16] : 0u;
+    uint32_t tot;
+    uint64_t pos = off[c] + sp_block_prefix((uint32_t)__popc(m), s_w, &tot);
+    if (x0 >= nb) return;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    uint8_t *b = (uint8_t *)&v;
+#pragma unroll
+    for (int q = 0; q < 16; q++)
+        if ((m >> q) & 1u) b[q] = pay[pos++];
+    if (x0 + 16 <= nb) {
+        *(uint4 *)(dst + x0) = v;
+    } else {
+        for (uint64_t x = x0; x < nb; x++) dst[x] = b[x - x0];
     }
 }
 

@@ -1676,6 +1676,13 @@ extern "C" int kh_group_counters(kh_group *grp, uint64_t *n_unique, uint64_t *n_
     });
 }
 
+extern "C" int kh_group_wire_stats(kh_group *grp, uint64_t *dense_bytes, uint64_t *sent_bytes) {
+    return guard([&] {
+        CHECK_PTR(grp);
+        group_wire_stats(grp->G, dense_bytes, sent_bytes);
+    });
+}
+
 extern "C" int kh_graph_get_bigcounts(kh_graph *h, uint64_t *keys, uint16_t *vals, uint64_t cap, uint64_t *n) {
     return guard([&] {
         CHECK_PTR(h);

@@ -1124,6 +1124,16 @@ static void winners_fine(Graph *g, PassState &ps) {
 // apply, crossing bins and the winner partition of a pass whose level-2
 // records are in place (fixed-capacity regions when l2f, else the exact
 // offsets off2)
+// The record-driven apply (k_apply_sparse) for the coarse-window path when
+// every region's capacity fits the APPLY_RECS records per thread of its 1024
+// threads (C4 / C5 / C5M regions: ~6-7K records); KH_SPARSE_APPLY=0 keeps
+// k_apply_count (read in every build: the tests compare both).
+static bool sparse_apply(const Graph *g, const PassState &ps, bool l2f) {
+    const bool on = test_env_int("KH_SPARSE_APPLY", 1) != 0;   // per pass: the tests toggle it
+    const Params &P = g->prm;
+    return on && ps.coarse && l2f && P.s0 == 14 && (P.kind == BYTE || P.kind == NIBBLE) &&
+           g->ws.reg_max + 2 <= (uint64_t)1024 * APPLY_RECS;
+}
 static void pass_apply(Graph *g, PassState &ps, bool l2f) {
     const Params &P = g->prm;
     Workspace &w = g->ws;
@@ -1196,7 +1206,18 @@ static void pass_apply(Graph *g, PassState &ps, bool l2f) {
     else if (P.kind == BIT)
         TIMED("apply_bit", hipLaunchKernelGGL(k_apply_bit<APPLY_THREADS>, dim3(agrid), dim3(APPLY_THREADS),
                                               lds_apply(P), st, P, A));
-    else if (P.kind == NIBBLE) {
+    else if (sparse_apply(g, ps, l2f)) {
+        // record-driven apply: every region's records fit the prefetch registers
+        const unsigned grid = (unsigned)std::min<uint64_t>(q.regions, device_cus(g));
+        const size_t lds = lds_apply_sparse((size_t)1 << P.s0);
+        using SpFn = void (*)(Params, ApplyArgs);
+        SpFn kn = ps.losers ? k_apply_sparse<NIBBLE, true> : k_apply_sparse<NIBBLE, false>;
+        SpFn kb = ps.losers ? k_apply_sparse<BYTE, true> : k_apply_sparse<BYTE, false>;
+        if (P.kind == NIBBLE)
+            TIMED("apply_nibble", hipLaunchKernelGGL(kn, dim3(grid), dim3(1024), lds, st, P, A));
+        else
+            TIMED("apply_byte", hipLaunchKernelGGL(kb, dim3(grid), dim3(1024), lds, st, P, A));
+    } else if (P.kind == NIBBLE) {
         TIMED("apply_nibble", hipLaunchKernelGGL(apply_count_kernel<NIBBLE>(P, ps.losers), dim3(agrid_count(g, q)),
                                                  dim3(apply_count_threads(P)), lds_apply(P), st, P, A));
     } else {
@@ -2100,6 +2121,10 @@ static void set_lds_limits() {
     (void)hipFuncSetAttribute((const void *)k_apply_count<BYTE, 512, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE, 512, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_count<BYTE, 1024, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_sparse<BYTE, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_sparse<BYTE, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_sparse<NIBBLE, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void *)k_apply_sparse<NIBBLE, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_count<NIBBLE, 1024, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_bit<APPLY_THREADS>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void *)k_apply_bit<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
@@ -2232,7 +2257,7 @@ Graph::~Graph() {
     void *ptrs[] = {d_tab, d_bc_keys, d_bc_vals, w.rec1, w.rec2, w.fullf, w.newbits, w.bc, w.bcn, w.bck, w.bcv,
                     w.off1, w.ch2, w.off2, w.mcnt, w.moff, w.scan_tmp, w.wcnt, w.xseg, w.reg_base, w.reg_cur, w.bkt_base, w.bkt_cur, w.ctr, w.d_words, w.d_koff, w.d_bytes,
                     w.q_hashes, w.q_counts, w.frec, w.fcount, w.d_rbytes, w.sm_flags, w.sm_hash, w.cw_cur, w.cmbase,
-                    w.cnk, w.wch, w.np_cur, w.np_blkj, w.np_fcur};
+                    w.cnk, w.wch, w.np_cur, w.np_blkj, w.np_fcur, w.sp_cnt, w.sp_off};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (w.h_ctr) (void)hipHostFree(w.h_ctr);
@@ -2319,6 +2344,10 @@ struct ShardGroup {
         uint64_t cap_o8 = 0;         // sharded query: the reduced minima of this rank's k-mers
         uint8_t *dbuf = nullptr;
         uint64_t cap_dbuf = 0;       // delta mode: every rank's delta (then prefix) of the owned slices
+        uint64_t *d_sz = nullptr;
+        uint64_t cap_dsz = 0;        // sparse delta pieces: payload sizes sent / received
+        uint8_t *stage = nullptr;
+        uint64_t cap_stage = 0;      // sparse delta pieces' staging when the dead record buffer is too small
         // hosted delta mode: the alltoallv's host staging, kept across passes
         // (about one table each way; only the slices' bytes are meaningful)
         std::vector<uint8_t> hsend, hrecv;
@@ -2327,6 +2356,7 @@ struct ShardGroup {
         bool freed[2] = {false, false};
     };
     std::vector<Local> loc;
+    uint64_t wire_dense = 0, wire_sent = 0;   // delta mode: bytes of the pieces between ranks, dense / as sent
     uint64_t *d_red = nullptr;
     std::vector<uint64_t> h_ws;      // [G][FJ+1]
     ~ShardGroup() {
@@ -2336,7 +2366,7 @@ struct ShardGroup {
             if (lc.st_x) (void)hipStreamSynchronize(lc.st_x);
             for (void *p : {(void *)lc.src, (void *)lc.recv, (void *)lc.ws, (void *)lc.ws_all, (void *)lc.roff,
                             (void *)lc.flist, (void *)lc.fall, (void *)lc.slot[0], (void *)lc.slot[1], (void *)lc.seg,
-                            (void *)lc.q8, (void *)lc.o8, (void *)lc.dbuf})
+                            (void *)lc.q8, (void *)lc.o8, (void *)lc.dbuf, (void *)lc.d_sz, (void *)lc.stage})
                 if (p) (void)hipFree(p);
             for (int b = 0; b < 2; b++) {
                 if (lc.ev_ready[b]) (void)hipEventDestroy(lc.ev_ready[b]);
@@ -3367,6 +3397,43 @@ static void delta_apply(Graph *V, PassState &ps, bool l2f) {
 
 // steps 2 and 4: forward = every rank's delta slices to their owners'
 // buffers; backward = every owner's prefix slices back into the ranks' views
+// Sparse pieces of the delta exchange (kh_apply.cuh k_sp_*): a table slice
+// travels as a bitmap of its nonzero bytes plus those bytes -- C4's deltas
+// are ~93 % zeros, so a rank-pass sends ~1/5 of the table bytes.
+// KH_DELTA_SPARSE=0 sends them dense (read in every build: the tests compare).
+static bool delta_sparse_on() { return test_env_int("KH_DELTA_SPARSE", 1) != 0; }
+static uint64_t sp_bm_bytes(uint64_t nb) { return ((nb + 15) / 16 * 2 + 15) & ~15ull; }
+static uint64_t sp_worst(uint64_t nb) { return sp_bm_bytes(nb) + ((nb + 15) & ~15ull); }
+static bool sp_aligned(const void *p) { return ((uintptr_t)p & 15) == 0; }
+// [src, src + nb) -> out (bitmap, then the payload at out + sp_bm_bytes(nb));
+// the payload's byte count into *d_size (device), on g's stream
+static void sp_pack(Graph *g, const uint8_t *src, uint64_t nb, uint8_t *out, uint64_t *d_size) {
+    Workspace &w = g->ws;
+    const uint64_t nch = (nb + SP_CHUNK - 1) / SP_CHUNK;
+    ensure((void **)&w.sp_cnt, &w.cap_spcnt, nch + 1, 4);
+    ensure((void **)&w.sp_off, &w.cap_spoff, nch + 1, 8);
+    KTimer kt_(g, "delta_pack");
+    hipLaunchKernelGGL(k_sp_count, dim3((unsigned)nch), dim3(SP_THREADS), 0, g->stream, src, nullptr, nb, w.sp_cnt);
+    scan_counts(g, w.sp_cnt, w.sp_off, nch + 1);
+    hipLaunchKernelGGL(k_sp_pack, dim3((unsigned)nch), dim3(SP_THREADS), 0, g->stream, src, nb, w.sp_off,
+                       (uint16_t *)out, out + sp_bm_bytes(nb));
+    KH_HIP(hipMemcpyAsync(d_size, w.sp_off + nch, 8, hipMemcpyDeviceToDevice, g->stream));
+    KH_HIP(hipGetLastError());
+}
+static void sp_unpack(Graph *g, const uint8_t *in, uint64_t nb, uint8_t *dst) {
+    Workspace &w = g->ws;
+    const uint64_t nch = (nb + SP_CHUNK - 1) / SP_CHUNK;
+    ensure((void **)&w.sp_cnt, &w.cap_spcnt, nch + 1, 4);
+    ensure((void **)&w.sp_off, &w.cap_spoff, nch + 1, 8);
+    KTimer kt_(g, "delta_unpack");
+    hipLaunchKernelGGL(k_sp_count, dim3((unsigned)nch), dim3(SP_THREADS), 0, g->stream, nullptr,
+                       (const uint16_t *)in, nb, w.sp_cnt);
+    scan_counts(g, w.sp_cnt, w.sp_off, nch + 1);
+    hipLaunchKernelGGL(k_sp_unpack, dim3((unsigned)nch), dim3(SP_THREADS), 0, g->stream, (const uint16_t *)in,
+                       in + sp_bm_bytes(nb), w.sp_off, nb, dst);
+    KH_HIP(hipGetLastError());
+}
+
 static void delta_exchange(ShardGroup *G, bool forward) {
     const int W = G->world, NL = G->nlocal, n = G->views[0]->n;
     std::vector<std::vector<uint64_t>> soff(W);
@@ -3387,6 +3454,84 @@ static void delta_exchange(ShardGroup *G, bool forward) {
             uint8_t *vt = V->d_tab + V->prm.tbyte[i] + b0;
             uint8_t *bt = lc.dbuf + (uint64_t)r * stride[r] + soff[r][i];
             KH_HIP(hipMemcpyAsync(forward ? bt : vt, forward ? vt : bt, nb, hipMemcpyDeviceToDevice, st));
+        }
+        // the pieces to and from every other rank: (table i of peer d) ->
+        // send src / receive dst and byte count, in (d, i) order
+        struct Piece { const uint8_t *src; uint8_t *dst; uint64_t nb; int d, i; };
+        std::vector<Piece> sends, recvs;
+        uint64_t need = 0;
+        bool aligned = true;
+        for (int d = 0; d < W; d++) {
+            if (d == r) continue;
+            for (int i = 0; i < n; i++) {
+                uint64_t b0, nb;
+                if (forward) {
+                    slice(d, i, &b0, &nb);
+                    if (nb) sends.push_back({V->d_tab + V->prm.tbyte[i] + b0, nullptr, nb, d, i});
+                    slice(r, i, &b0, &nb);
+                    if (nb) recvs.push_back({nullptr, lc.dbuf + (uint64_t)d * stride[r] + soff[r][i], nb, d, i});
+                } else {
+                    slice(r, i, &b0, &nb);
+                    if (nb) sends.push_back({lc.dbuf + (uint64_t)d * stride[r] + soff[r][i], nullptr, nb, d, i});
+                    slice(d, i, &b0, &nb);
+                    if (nb) recvs.push_back({nullptr, V->d_tab + V->prm.tbyte[i] + b0, nb, d, i});
+                }
+            }
+        }
+        for (const Piece &p : sends) { need += sp_worst(p.nb); aligned = aligned && sp_aligned(p.src); }
+        for (const Piece &p : recvs) { need += sp_worst(p.nb); aligned = aligned && sp_aligned(p.dst); }
+        // staging: the view's level-1 record buffer (dead between level 2 and
+        // the apply that follows the exchange)
+        if (!sends.empty() && delta_sparse_on() && aligned) {
+            uint8_t *stage = (uint8_t *)V->ws.rec1;
+            if (need > V->ws.cap_recs * 8) {
+                ensure((void **)&lc.stage, &lc.cap_stage, need, 1);
+                stage = lc.stage;
+            }
+            ensure((void **)&lc.d_sz, &lc.cap_dsz, 2 * (uint64_t)W * n, 8);
+            uint64_t *d_ssz = lc.d_sz, *d_rsz = lc.d_sz + (uint64_t)W * n;
+            KH_HIP(hipMemsetAsync(lc.d_sz, 0, 2 * (uint64_t)W * n * 8, st));
+            std::vector<uint64_t> sb(sends.size()), rb(recvs.size());
+            uint64_t at = 0;
+            for (size_t k = 0; k < sends.size(); k++) {
+                sb[k] = at;
+                at += sp_worst(sends[k].nb);
+                sp_pack(V, sends[k].src, sends[k].nb, stage + sb[k], d_ssz + (uint64_t)sends[k].d * n + sends[k].i);
+            }
+            for (size_t k = 0; k < recvs.size(); k++) {
+                rb[k] = at;
+                at += sp_worst(recvs[k].nb);
+            }
+            // payload sizes first (n per peer), then the pieces
+            KH_NCCL(ncclGroupStart());
+            for (int d = 0; d < W; d++) {
+                if (d == r) continue;
+                KH_NCCL(ncclSend(d_ssz + (uint64_t)d * n, n, ncclUint64, d, G->comm, st));
+                KH_NCCL(ncclRecv(d_rsz + (uint64_t)d * n, n, ncclUint64, d, G->comm, st));
+            }
+            KH_NCCL(ncclGroupEnd());
+            std::vector<uint64_t> hsz(2 * (uint64_t)W * n);
+            KH_HIP(hipMemcpyAsync(hsz.data(), lc.d_sz, hsz.size() * 8, hipMemcpyDeviceToHost, st));
+            KH_HIP(hipStreamSynchronize(st));
+            KH_NCCL(ncclGroupStart());
+            for (size_t k = 0; k < sends.size(); k++) {
+                const uint64_t bytes = sp_bm_bytes(sends[k].nb) + hsz[(uint64_t)sends[k].d * n + sends[k].i];
+                G->wire_dense += sends[k].nb;
+                G->wire_sent += bytes;
+                KH_NCCL(ncclSend(stage + sb[k], bytes, ncclUint8, sends[k].d, G->comm, st));
+            }
+            for (size_t k = 0; k < recvs.size(); k++) {
+                const uint64_t sz = hsz[(uint64_t)W * n + (uint64_t)recvs[k].d * n + recvs[k].i];
+                if (sz > recvs[k].nb) fail(KH_EDEVICE, "sparse delta piece larger than its slice");
+                KH_NCCL(ncclRecv(stage + rb[k], sp_bm_bytes(recvs[k].nb) + sz, ncclUint8, recvs[k].d, G->comm, st));
+            }
+            KH_NCCL(ncclGroupEnd());
+            for (size_t k = 0; k < recvs.size(); k++) sp_unpack(V, stage + rb[k], recvs[k].nb, recvs[k].dst);
+            return;
+        }
+        for (const Piece &p : sends) {
+            G->wire_dense += p.nb;
+            G->wire_sent += p.nb;
         }
         KH_NCCL(ncclGroupStart());
         for (int d = 0; d < W; d++) {
@@ -3461,7 +3606,10 @@ static void delta_exchange(ShardGroup *G, bool forward) {
         }
         return;
     }
-    // loopback: device copies between the local views and owners
+    // loopback: device copies between the local views and owners; pieces
+    // between two ranks of one device go through the sparse codec, as they
+    // would on the wire (packed into the owner's dead level-1 buffer and
+    // unpacked from it, one piece at a time on the owner's stream)
     for (int l = 0; l < NL; l++) KH_HIP(hipStreamSynchronize(G->views[l]->stream));
     for (int o = 0; o < W; o++) {
         auto &lc = G->loc[o];
@@ -3475,7 +3623,29 @@ static void delta_exchange(ShardGroup *G, bool forward) {
                 if (!nb) continue;
                 uint8_t *vt = Vs->d_tab + Vs->prm.tbyte[i] + b0;
                 uint8_t *bt = lc.dbuf + (uint64_t)s * stride[o] + soff[o][i];
-                KH_HIP(hipMemcpyAsync(forward ? bt : vt, forward ? vt : bt, nb, hipMemcpyDefault, Vo->stream));
+                const uint8_t *src = forward ? vt : bt;
+                uint8_t *dst = forward ? bt : vt;
+                if (s != o && delta_sparse_on() && Vs->device == Vo->device && sp_aligned(src) && sp_aligned(dst)) {
+                    uint8_t *stage = (uint8_t *)Vo->ws.rec1;
+                    if (sp_worst(nb) > Vo->ws.cap_recs * 8) {
+                        ensure((void **)&lc.stage, &lc.cap_stage, sp_worst(nb), 1);
+                        stage = lc.stage;
+                    }
+                    ensure((void **)&lc.d_sz, &lc.cap_dsz, 2, 8);
+                    sp_pack(Vo, src, nb, stage, lc.d_sz);
+                    sp_unpack(Vo, stage, nb, dst);
+                    uint64_t sz = 0;
+                    KH_HIP(hipMemcpyAsync(&sz, lc.d_sz, 8, hipMemcpyDeviceToHost, Vo->stream));
+                    KH_HIP(hipStreamSynchronize(Vo->stream));
+                    G->wire_dense += nb;
+                    G->wire_sent += sp_bm_bytes(nb) + sz;
+                    continue;
+                }
+                if (s != o) {
+                    G->wire_dense += nb;
+                    G->wire_sent += nb;
+                }
+                KH_HIP(hipMemcpyAsync(dst, src, nb, hipMemcpyDefault, Vo->stream));
             }
         }
     }
@@ -3996,6 +4166,11 @@ void group_median_fixed(ShardGroup *G, const void *const *d_reads, uint64_t nrea
         engine_collect_events(g);
     }
     for (Graph *V : G->views) KH_HIP(hipStreamSynchronize(V->stream));
+}
+
+void group_wire_stats(const ShardGroup *G, uint64_t *dense_bytes, uint64_t *sent_bytes) {
+    if (dense_bytes) *dense_bytes = G->wire_dense;
+    if (sent_bytes) *sent_bytes = G->wire_sent;
 }
 
 // n_unique / n_occupied of the whole group (collective in RCCL mode)

@@ -158,6 +158,10 @@ struct Workspace {
     // the fine records (kh_nearprime.cuh k_scatter_n1b)
     unsigned long long *np_fcur = nullptr;
     uint64_t cap_npfcur = 0;
+    // sparse delta pieces (kh_engine.hip sp_pack / sp_unpack): chunk counts, offsets
+    uint32_t *sp_cnt = nullptr;
+    uint64_t *sp_off = nullptr;
+    uint64_t cap_spcnt = 0, cap_spoff = 0;
     double reg_sigma = 0, bkt_sigma = 0;          // capacity margins the plans were made with
     // fixed-capacity level 1 (k_scatter_l1f): bucket b holds [bkt_base[b], bkt_cur[b])
     uint64_t *bkt_base = nullptr, *bkt_cur = nullptr;
@@ -406,6 +410,7 @@ void group_consume_bytes_fixed(ShardGroup *G, const uint8_t *const *d_bytes, uin
 void group_median_fixed(ShardGroup *G, const void *const *d_reads, uint64_t nreads, uint64_t read_len,
                         uint16_t *const *d_med, float *const *d_avg, float *const *d_sd);
 void group_counters(ShardGroup *G, uint64_t *n_unique, uint64_t *n_occupied);
+void group_wire_stats(const ShardGroup *G, uint64_t *dense_bytes, uint64_t *sent_bytes);
 int group_world(ShardGroup *G);
 int group_nlocal(ShardGroup *G);
 int group_rank(ShardGroup *G, int l);

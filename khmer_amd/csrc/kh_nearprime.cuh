@@ -348,8 +348,11 @@ __global__ void __launch_bounds__(THREADS) k_scatter_n2(NPGeo N, uint32_t parts,
                                                         const uint32_t *blkj, int blk_sh1, const uint64_t *reg_base,
                                                         unsigned long long *reg_cur, const uint64_t *rec_in,
                                                         uint64_t *rec_out, uint64_t *ctr, int blk_sh) {
-    constexpr int RPT = 8;
-    constexpr int IN = NT == 2 ? 4 : 2;   // level-1 records per thread a tile
+#ifndef KH_N2_IN
+#define KH_N2_IN 2   // development A/B: level-1 records per thread a tile at 3-4 tables
+#endif
+    constexpr int IN = NT == 2 ? 2 * KH_N2_IN : KH_N2_IN;   // level-1 records per thread a tile
+    constexpr int RPT = IN * NT <= 8 ? 8 : IN * NT;
     constexpr int TILE = THREADS * IN;
     constexpr uint32_t SEG = 16;
     static_assert(NT >= 2 && NT <= NP_MAXT && IN * NT <= RPT, "k_scatter_n2: 2 to 4 tables");

@@ -372,6 +372,13 @@ class ShardedGraph(object):
         check(lib.kh_group_counters(self._h, ctypes.byref(u), ctypes.byref(o)))
         return u.value, o.value
 
+    def wire_stats(self):
+        """Delta mode: (dense, sent) bytes of the table pieces exchanged with
+        other ranks so far (sparse pieces: bitmap + nonzero bytes)."""
+        d, t = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib.kh_group_wire_stats(self._h, ctypes.byref(d), ctypes.byref(t)))
+        return d.value, t.value
+
     def local_tables(self):
         """[[slice bytes per table] per local shard]."""
         return [[s.table_bytes(i) for i in range(len(self.sizes))] for s in self.shards]

@@ -102,3 +102,18 @@ def test_compare_fixture(bench):
 def test_algorithmic_bytes(bench):
     assert abs(bench.algorithmic_bytes_per_kmer(150, 21, 4) - 8.288461538) < 1e-6
     assert abs(bench.query_bytes_per_kmer(150, 51, 4) - 4.475) < 1e-9
+
+
+@pytest.mark.parametrize("argv,mode", [
+    ([], "delta"),
+    (["--gpus", "8"], "delta"),                                  # C2 weak: 4 GB vs 3.25e9 k-mers a rank-pass
+    (["--gpus", "8", "--strong"], "delta"),                      # C2 strong: 4 GB vs 0.8e9 k-mers
+    (["--gpus", "8", "--config", "C4"], "delta"),                # C4 weak: 32 GB vs 3.25e9 k-mers
+    (["--gpus", "8", "--config", "C4", "--strong"], "exchange"), # C4 strong: 32 GB vs 0.8e9 k-mers
+    (["--gpus", "8", "--config", "C4", "--strong", "--group-mode", "delta"], "delta"),
+])
+def test_auto_group_mode(bench, argv, mode):
+    """bench.py picks the group mode per configuration from the
+    crossover DESIGN.md §6 derives (table bytes against 4 x tables x the
+    k-mers of a rank-pass); an explicit --group-mode wins."""
+    assert _args(bench, argv).group_mode == mode

@@ -143,6 +143,29 @@ def test_loopback_delta_saturated_bigcount(world):
     g.close()
 
 
+@pytest.mark.parametrize("sparse", ["1", "0"], ids=["sparse", "dense"])
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("cls,k", [("Countgraph", 21), ("SmallCountgraph", 21), ("Nodegraph", 31)])
+def test_loopback_delta_sparse_pieces(cls, k, world, sparse, monkeypatch):
+    """Delta mode's pieces between ranks as bitmap + nonzero bytes
+    (KH_DELTA_SPARSE, kh_apply.cuh k_sp_*): tables sized so each rank's
+    chunk touches a few % of the bins (as C4's passes do), several passes.
+    Tables, counters and bigcounts equal the oracle's either way; sparse
+    pieces carry a fraction of the slice bytes (the group's wire counters)."""
+    monkeypatch.setenv("KH_DELTA_SPARSE", sparse)
+    sizes = O.get_n_primes_near_x(4, 8000009)
+    g, o = run_pair(cls, k, sizes, world, nreads=3000, L=150, batch=1 << 17, bigcount=(cls == "Countgraph"),
+                    mode="delta")
+    assert_group_equals_oracle(g, o, sizes, cls == "Countgraph")
+    dense, sent = g.wire_stats()
+    assert dense > 0
+    if sparse == "1":
+        assert sent < dense * 0.5, (dense, sent)
+    else:
+        assert sent == dense
+    g.close()
+
+
 def test_exchange_slices_are_bucket_ranges():
     """Exchange-mode ownership: contiguous, covering, byte-aligned slices that
     start on level-1 bucket boundaries (a rank may own nothing of a table)."""
