@@ -3480,6 +3480,27 @@ static void delta_exchange(ShardGroup *G, bool forward) {
         }
         for (const Piece &p : sends) { need += sp_worst(p.nb); aligned = aligned && sp_aligned(p.src); }
         for (const Piece &p : recvs) { need += sp_worst(p.nb); aligned = aligned && sp_aligned(p.dst); }
+        // KH_DELTA_PROBE=1 at world 1 (tools/rank_model.py): no piece leaves
+        // the rank, so pack the own slices instead and count them, for the
+        // sparse wire estimate of a larger group
+        // (the deltas only: the prefixes of a larger group are denser than a
+        // world-1 rank's, which is the table before the pass)
+        if (forward && sends.empty() && W == 1 && test_env_int("KH_DELTA_PROBE", 0)) {
+            ensure((void **)&lc.d_sz, &lc.cap_dsz, 2, 8);
+            for (int i = 0; i < n; i++) {
+                uint64_t b0, nb;
+                slice(r, i, &b0, &nb);
+                const uint8_t *src = V->d_tab + V->prm.tbyte[i] + b0;
+                if (!nb || !sp_aligned(src)) continue;
+                ensure((void **)&lc.stage, &lc.cap_stage, sp_worst(nb), 1);
+                sp_pack(V, src, nb, lc.stage, lc.d_sz);
+                uint64_t sz = 0;
+                KH_HIP(hipMemcpyAsync(&sz, lc.d_sz, 8, hipMemcpyDeviceToHost, st));
+                KH_HIP(hipStreamSynchronize(st));
+                G->wire_dense += nb;
+                G->wire_sent += std::min(sp_bm_bytes(nb) + sz, nb);
+            }
+        }
         // staging: the view's level-1 record buffer (dead between level 2 and
         // the apply that follows the exchange)
         if (!sends.empty() && delta_sparse_on() && aligned) {
@@ -3514,19 +3535,31 @@ static void delta_exchange(ShardGroup *G, bool forward) {
             KH_HIP(hipMemcpyAsync(hsz.data(), lc.d_sz, hsz.size() * 8, hipMemcpyDeviceToHost, st));
             KH_HIP(hipStreamSynchronize(st));
             KH_NCCL(ncclGroupStart());
+            // a piece whose sparse form is not smaller travels dense (both
+            // sides decide from the same payload size)
+            std::vector<char> rsparse(recvs.size(), 0);
             for (size_t k = 0; k < sends.size(); k++) {
                 const uint64_t bytes = sp_bm_bytes(sends[k].nb) + hsz[(uint64_t)sends[k].d * n + sends[k].i];
                 G->wire_dense += sends[k].nb;
-                G->wire_sent += bytes;
-                KH_NCCL(ncclSend(stage + sb[k], bytes, ncclUint8, sends[k].d, G->comm, st));
+                G->wire_sent += std::min(bytes, sends[k].nb);
+                if (bytes < sends[k].nb)
+                    KH_NCCL(ncclSend(stage + sb[k], bytes, ncclUint8, sends[k].d, G->comm, st));
+                else
+                    KH_NCCL(ncclSend(sends[k].src, sends[k].nb, ncclUint8, sends[k].d, G->comm, st));
             }
             for (size_t k = 0; k < recvs.size(); k++) {
                 const uint64_t sz = hsz[(uint64_t)W * n + (uint64_t)recvs[k].d * n + recvs[k].i];
                 if (sz > recvs[k].nb) fail(KH_EDEVICE, "sparse delta piece larger than its slice");
-                KH_NCCL(ncclRecv(stage + rb[k], sp_bm_bytes(recvs[k].nb) + sz, ncclUint8, recvs[k].d, G->comm, st));
+                const uint64_t bytes = sp_bm_bytes(recvs[k].nb) + sz;
+                rsparse[k] = bytes < recvs[k].nb;
+                if (rsparse[k])
+                    KH_NCCL(ncclRecv(stage + rb[k], bytes, ncclUint8, recvs[k].d, G->comm, st));
+                else
+                    KH_NCCL(ncclRecv(recvs[k].dst, recvs[k].nb, ncclUint8, recvs[k].d, G->comm, st));
             }
             KH_NCCL(ncclGroupEnd());
-            for (size_t k = 0; k < recvs.size(); k++) sp_unpack(V, stage + rb[k], recvs[k].nb, recvs[k].dst);
+            for (size_t k = 0; k < recvs.size(); k++)
+                if (rsparse[k]) sp_unpack(V, stage + rb[k], recvs[k].nb, recvs[k].dst);
             return;
         }
         for (const Piece &p : sends) {
@@ -3633,12 +3666,16 @@ static void delta_exchange(ShardGroup *G, bool forward) {
                     }
                     ensure((void **)&lc.d_sz, &lc.cap_dsz, 2, 8);
                     sp_pack(Vo, src, nb, stage, lc.d_sz);
-                    sp_unpack(Vo, stage, nb, dst);
                     uint64_t sz = 0;
                     KH_HIP(hipMemcpyAsync(&sz, lc.d_sz, 8, hipMemcpyDeviceToHost, Vo->stream));
                     KH_HIP(hipStreamSynchronize(Vo->stream));
                     G->wire_dense += nb;
-                    G->wire_sent += sp_bm_bytes(nb) + sz;
+                    G->wire_sent += std::min(sp_bm_bytes(nb) + sz, nb);
+                    if (sp_bm_bytes(nb) + sz < nb) {   // else dense, as on the wire
+                        sp_unpack(Vo, stage, nb, dst);
+                        continue;
+                    }
+                    KH_HIP(hipMemcpyAsync(dst, src, nb, hipMemcpyDefault, Vo->stream));
                     continue;
                 }
                 if (s != o) {

@@ -249,7 +249,8 @@ __global__ void __launch_bounds__(L1_THREADS, L1F_WAVES_PER_EU) k_scatter_n1(NPG
                     }
                 }
                 const uint32_t fe = (last || stale) ? e : (e & ~1u);
-                if ((L0 & 1) && fe > L0 - 1 && bc != NP_DEAD) rec[(uint64_t)d * CAP + bc + ((L0 - 1) & (BLK - 1))] = tail[d];
+                if ((L0 & 1) && fe > L0 - 1 && bc != NP_DEAD && !(KH_ABL(N, 16)))   // 16: the tails were never written
+                    rec[(uint64_t)d * CAP + bc + ((L0 - 1) & (BLK - 1))] = tail[d];
                 const uint32_t q0 = lstart[d];
                 if (h) {
                     if (L0 & 1) slot[q0 - 1] = ((uint64_t)d << NP_SLOT_B) | ((uint64_t)NP_EMPTY << NP_SLOT_K);

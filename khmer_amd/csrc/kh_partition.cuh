@@ -739,7 +739,7 @@ __global__ void __launch_bounds__(L1_THREADS, RPT_ == 8 ? L1F_WAVES_PER_EU : 4) 
                 }
             }
             const uint32_t e = L0 + h, fe = last ? e : (e & ~1u);
-            if ((L0 & 1) && fe > L0 - 1 && bc != DEAD) rec[bc + ((L0 - 1) & (BLK - 1))] = tail[d];
+            if ((L0 & 1) && fe > L0 - 1 && bc != DEAD && !(KH_ABL(P, 16))) rec[bc + ((L0 - 1) & (BLK - 1))] = tail[d];   // 16: the tails were never written
             const uint32_t q0 = lstart[d];   // the run's first slot (odd after a hole)
             if (h) {
                 if (L0 & 1) slot[q0 - 1] = (uint64_t)((d << 16) | SLOT_EMPTY) << 32;
@@ -1024,7 +1024,7 @@ __global__ void __launch_bounds__(L1_THREADS, L1F_WAVES_PER_EU) k_scatter_l1p(Pa
                     }
                 }
                 const uint32_t e = L0 + h, fe = last ? e : (e & ~1u);
-                if ((L0 & 1) && fe > L0 - 1 && bc != DEAD) rec[bc + ((L0 - 1) & (BLK - 1))] = tail[d];
+                if ((L0 & 1) && fe > L0 - 1 && bc != DEAD && !(KH_ABL(P, 16))) rec[bc + ((L0 - 1) & (BLK - 1))] = tail[d];   // 16: the tails were never written
                 const uint32_t q0 = lstart[d];
                 if (h) {
                     if (L0 & 1) slot[q0 - 1] = (uint64_t)((d << 16) | SLOT_EMPTY) << 32;

@@ -11,7 +11,11 @@ the tables (the table's bytes in all) -- so the world-1 kernel times ARE the
 per-rank compute at any G.  Exchange mode's passes shrink with G (a pass takes
 batch / G k-mers of every rank), so it runs at batch / G here.  The wire time
 is not measured (one GPU): the bytes a rank sends over xGMI per step are
-stated, with the time they take at an assumed per-GPU one-way rate.
+stated, with the time they take at an assumed per-GPU one-way rate.  Delta
+mode's pieces travel sparse (bitmap + nonzero bytes, kh_engine.hip
+sp_pack): KH_DELTA_PROBE=1 packs the world-1 rank's own delta slices to
+measure their sparse size; the estimate keeps the prefixes dense (an upper
+bound: a rank's prefix at G > 1 is denser than the world-1 table).
 
     python tools/rank_model.py --mode delta --world 8 [--config C2|C4] [--reads 50000000]
 Prints one JSON line."""
@@ -39,6 +43,7 @@ def main():
     ap.add_argument("--xgmi-gbs", type=float, default=350.0,
                     help="assumed one-way xGMI rate per GPU for the wire estimate (7 links x ~50 GB/s)")
     a = ap.parse_args()
+    os.environ["KH_DELTA_PROBE"] = "1"
     import khmer_amd
     from khmer_amd import parallel, synth
     from khmer_amd._lib import lib, check
@@ -85,13 +90,22 @@ def main():
         wire = 8 * nt * kmers * (W - 1) / W                # level-1 records to their owners
     wire_ms = wire / (a.xgmi_gbs * 1e9) * 1e3
     u, occ = g.counters()
+    sparse = {}
+    if a.mode == "delta":
+        dense_b, sent_b = g.wire_stats()   # the probe's own delta slices, every pass of the warmup + timed steps
+        if dense_b:
+            ratio = sent_b / dense_b
+            wire_sp = wire / 2 * ratio + wire / 2   # deltas sparse, prefixes dense
+            sparse = {"delta_sparse_ratio": round(ratio, 4), "wire_bytes_sparse_per_rank_step": wire_sp,
+                      "wire_ms_sparse_at_assumed_rate": round(wire_sp / (a.xgmi_gbs * 1e9) * 1e3, 1),
+                      "rank_step_ms_sparse_unoverlapped": round(dt * 1e3 + wire_sp / (a.xgmi_gbs * 1e9) * 1e3, 1)}
     out = {"mode": a.mode, "world_modelled": W, "config": a.config, "reads_per_rank": a.reads,
            "kmers_per_rank": kmers, "passes_per_step": npass, "batch_kmers": batch,
            "compute_ms_per_rank_step": round(dt * 1e3, 2), "kernels_ms_per_step": kern,
            "wire_bytes_per_rank_step": wire, "wire_bytes_per_kmer": wire / kmers,
            "wire_ms_at_assumed_rate": round(wire_ms, 1), "assumed_xgmi_gbs_one_way": a.xgmi_gbs,
            "rank_step_ms_unoverlapped": round(dt * 1e3 + wire_ms, 1),
-           "n_unique": u, "n_occupied": occ}
+           "n_unique": u, "n_occupied": occ, **sparse}
     print(json.dumps(out), flush=True)
     lib.kh_device_free(0, words)
     lib.kh_device_free(0, koff)
