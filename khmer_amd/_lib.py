@@ -117,6 +117,8 @@ SIGNATURES = {
 }
 
 for _name, (_res, _args) in SIGNATURES.items():
+    if os.environ.get("KHMER_AMD_LIB") and not hasattr(lib, _name):
+        continue   # an older development build (A/B runs) may lack newer entry points
     _fn = getattr(lib, _name)
     _fn.restype = _res
     _fn.argtypes = _args

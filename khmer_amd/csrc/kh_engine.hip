@@ -1127,7 +1127,9 @@ static void winners_fine(Graph *g, PassState &ps) {
 // The record-driven apply (k_apply_sparse) for the coarse-window path when
 // every region's capacity fits the APPLY_RECS records per thread of its 1024
 // threads (C4 / C5 / C5M regions: ~6-7K records); KH_SPARSE_APPLY=0 keeps
-// k_apply_count (read in every build: the tests compare both).
+// k_apply_count (read in every build: the tests compare both).  A Bit
+// variant (16 records a thread, C3's ~12K a region) measured slower than
+// k_apply_bit (142 vs 115 ms/step) and was removed.
 static bool sparse_apply(const Graph *g, const PassState &ps, bool l2f) {
     const bool on = test_env_int("KH_SPARSE_APPLY", 1) != 0;   // per pass: the tests toggle it
     const Params &P = g->prm;
