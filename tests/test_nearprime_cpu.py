@@ -11,7 +11,10 @@ i * Rloc + (its region - R' b) (+ table i's regions when it wrapped).  This
 test walks edge hashes (0, 4^k - 1, multiples of P and of every p_i +- 1,
 bucket boundaries, wrap-around) and random ones through that arithmetic for
 the C2 / C4 geometries and checks the bins, the destination range, the
-record bit layout and the bucket magic."""
+record bit layout and the bucket magic.  Tables past 256 level-1 buckets (C4)
+take three levels: k_scatter_n1b splits each coarse bucket into F fine ones
+and rewrites the record as j << 32 | q << ob_f | offset; the same bins come
+out of level 2 over the fine geometry."""
 import random
 
 import pytest
@@ -60,8 +63,10 @@ def ceil_log2(x):
     return s
 
 
-def np_geometry(sizes, k, span_bits=24):
-    """np_geometry (kh_engine.hip) restated; None when the path is not taken."""
+def np_geometry(sizes, k, span_bits=24, lim=256):
+    """np_geometry (kh_engine.hip) restated; None when the path is not taken.
+    More than `lim` level-1 buckets: three levels (G["F"] fine buckets of
+    G["rpf"] regions a coarse bucket of G["rp"] = F x rpf regions)."""
     n = len(sizes)
     if not 2 <= n <= 4 or k > 26:
         return None
@@ -82,10 +87,22 @@ def np_geometry(sizes, k, span_bits=24):
     E = (maxoff + R - 1) >> S0
     if E + 1 >= rloc // 2:
         return None
-    rp = rloc - E - 1
+    rpf = rloc - E - 1
     Rm = (pm + R - 1) >> S0
+    F, rp1, fine = 1, rpf, None
+    if (Rm + rpf - 1) // rpf > lim:   # three levels
+        qb = ceil_log2(qmax + 1)
+        if qb + S0 + 1 > 32:
+            return None
+        rp1 = min(rpf, ((1 << (32 - qb)) - 1) // R)
+        F = (Rm + rp1 * lim - 1) // (rp1 * lim)
+        obf = ceil_log2(rp1 * R + 1)
+        if F > 16 or obf + qb > 32:
+            return None
+        fine = dict(F=F, rp=rp1, ob=obf, magic=((1 << 32) + rp1 - 1) // rp1, rloc=rp1 + E + 1)
+    rp = rp1 * F
     nb = (Rm + rp - 1) // rp
-    if nb > 256:
+    if nb > lim:
         return None
     ob = ceil_log2(rp * R + 1)
     pb = ob + ceil_log2(qmax + 1)
@@ -93,7 +110,28 @@ def np_geometry(sizes, k, span_bits=24):
         return None
     magic = ((1 << 32) + rp - 1) // rp
     return dict(n=n, pm=pm, d=d, p=list(sizes), qmax=qmax, rloc=rloc, rp=rp, nb=nb, ob=ob, pb=pb, magic=magic,
-                rt=[(p + R - 1) >> S0 for p in sizes], rbase=[t >> S0 for t in tbase], Rm=Rm, E=E)
+                rt=[(p + R - 1) >> S0 for p in sizes], rbase=[t >> S0 for t in tbase], Rm=Rm, E=E, fine=fine)
+
+
+def fine_geometry(G):
+    """np_fine_geo: level 2's view of a three-level partition."""
+    f = G["fine"]
+    H = dict(G)
+    H.update(rp=f["rp"], magic=f["magic"], nb=G["nb"] * f["F"], ob=f["ob"], pb=32, rloc=f["rloc"], fine=None)
+    return H
+
+
+def level1b(G, b, pay, j):
+    """k_scatter_n1b: coarse bucket b's record -> (fine bucket, fine record)."""
+    f = G["fine"]
+    q, off = pay >> G["ob"], pay & ((1 << G["ob"]) - 1)
+    fb = ((off >> S0) * f["magic"]) >> 32
+    assert fb < f["F"] and fb == (off >> S0) // f["rp"]
+    offf = off - fb * (f["rp"] << S0)
+    assert 0 <= offf < f["rp"] << S0
+    rec = (j << 32) | (q << f["ob"]) | offf
+    assert (q << f["ob"]) | offf < 1 << 32 and rec != (1 << 64) - 1
+    return b * f["F"] + fb, rec & 0xFFFFFFFF
 
 
 def level1(G, h):
@@ -163,12 +201,15 @@ def test_bins_equal_per_table_modulo(x, k, expect_nb):
         assert (G["qmax"], G["rp"], G["ob"], G["pb"]) == (4398, 240, 22, 35)
     rnd = random.Random(int(x) ^ k)
     hs = edge_hashes(G, k, rnd, 3000)
+    H = fine_geometry(G) if G["fine"] else G
     for h in hs:
         b, pay = level1(G, h)
         assert b < G["nb"]
-        for i, (dst, greg, off, bin_) in enumerate(level2(G, b, pay)):
+        if G["fine"]:   # three levels (tables past 256 buckets: C4's 8e9, 2e9)
+            b, pay = level1b(G, b, pay, j=7)
+        for i, (dst, greg, off, bin_) in enumerate(level2(H, b, pay)):
             assert bin_ == h % G["p"][i]
-            assert dst < G["n"] * G["rloc"] <= 1024
+            assert dst < H["n"] * H["rloc"] <= 1024
 
 
 def test_bucket_magic_exact():
@@ -198,3 +239,35 @@ def test_record_layout_and_span():
     assert jbits == 29 and (1 << jbits) - 1 >= 4096 * 32
     worst = (((1 << jbits) - 1) << G["pb"]) | (G["qmax"] << G["ob"]) | (G["rp"] * R - 1)
     assert worst != (1 << 64) - 1
+
+
+@pytest.mark.parametrize("x,k,lim,expect", [(8e9, 21, 256, (8, 242, 253)), (1e8, 19, 8, (13, 8, 63)),
+                                            (1e9, 21, 128, (16, 124, 31))])
+def test_three_level_bins_equal_per_table_modulo(x, k, lim, expect):
+    """C4 (and the GPU tests' KH_NP_L1MAX geometries): level 1 into coarse
+    buckets, level 1b into fine ones (q and the offset in 32 bits beside the
+    pass index), level 2 from the fine record -- every table's bin is still
+    h % p_i and every destination is inside the fine bucket's range."""
+    G = np_geometry(primes_near(4, x), k, lim=lim)
+    assert G is not None and G["fine"] is not None
+    assert (G["fine"]["F"], G["nb"], G["fine"]["rp"]) == expect
+    H = fine_geometry(G)
+    assert H["n"] * H["rloc"] <= 1024
+    rnd = random.Random(int(x) ^ k ^ lim)
+    hs = edge_hashes(G, k, rnd, 2000) + edge_hashes(H, k, rnd, 0)
+    for h in hs:
+        b, pay = level1(G, h)
+        assert b < G["nb"]
+        fb, fpay = level1b(G, b, pay, j=12345)
+        for i, (dst, greg, off, bin_) in enumerate(level2(H, fb, fpay)):
+            assert bin_ == h % G["p"][i]
+            assert dst < H["n"] * H["rloc"]
+
+
+def test_three_level_magic_exact():
+    G = np_geometry(primes_near(4, 8e9), 21)
+    f = G["fine"]
+    for rho in range(G["Rm"]):
+        assert (rho * G["magic"]) >> 32 == rho // G["rp"]
+    for rho in range(G["rp"]):
+        assert (rho * f["magic"]) >> 32 == rho // f["rp"]
